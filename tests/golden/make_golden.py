@@ -1,0 +1,386 @@
+"""Generate the committed golden fixtures by running the REFERENCE itself (build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [/root/reference]
+
+The reference is imported read-only from its checkout (libs.uvit, libs.uvit_t2i,
+libs.autoencoder, dpm_solver_pytorch import directly; dpm_solver_pp needs a stub for its unused
+`import utils`; sde needs a stub for `absl.logging`).  Small helpers that live in un-importable modules
+(utils.int2bits / bits2int / amortize, datasets unpreprocess) are executed from the reference source with
+`ast` so their outputs come from the reference's own code.
+
+Inputs are produced by this repo's seeded generators (panopticdiffusionmodels_amd.weights and
+`_inputs` below), so only outputs + input checksums are stored.  Nothing here is imported by the product
+or run on the GPU box; the .npz files are data.
+"""
+import ast
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from panopticdiffusionmodels_amd import configs as C  # noqa: E402
+from panopticdiffusionmodels_amd import weights as W  # noqa: E402
+
+
+def _import_reference(ref):
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, ref)
+    sys.modules.setdefault("utils", types.ModuleType("utils"))  # dpm_solver_pp.py:6 (unused)
+    absl = types.ModuleType("absl")
+    logging = types.ModuleType("absl.logging")
+    logging.info = logging.debug = logging.warning = lambda *a, **k: None
+    absl.logging = logging
+    sys.modules.setdefault("absl", absl)
+    sys.modules.setdefault("absl.logging", logging)
+    import libs.uvit as uvit
+    import libs.uvit_t2i as uvit_t2i
+    import libs.autoencoder as ae
+    import dpm_solver_pp as pp
+    import dpm_solver_pytorch as dpt
+    import sde
+    return uvit, uvit_t2i, ae, pp, dpt, sde
+
+
+def _ref_funcs(path, names):
+    """Execute selected top-level functions from a reference source file that cannot be imported whole."""
+    src = open(path).read()
+    tree = ast.parse(src)
+    keep = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in names]
+    mod = ast.Module(body=keep, type_ignores=[])
+    ns = {"torch": torch, "np": np}
+    exec(compile(mod, path, "exec"), ns)
+    return {n: ns[n] for n in names}
+
+
+def _inputs(cfg_name, B, seed):
+    """Seeded model inputs (same generator the tests use)."""
+    cfg = C.get_config(cfg_name)
+    n = cfg["nnet"]
+    g = torch.Generator().manual_seed(seed)
+    Cc, H, Wd = cfg["z_shape"]
+    out = {"x": torch.randn(B, Cc, H, Wd, generator=g),
+           "t": torch.rand(B, generator=g) * 998.0 + 1.0}
+    if n["name"] == "uvit" and n.get("num_classes", -1) > 0:
+        y = torch.randint(0, n["num_classes"] - 1, (B,), generator=g)
+        y[-1] = n["num_classes"] - 1  # the null label
+        out["y"] = y
+    if n["name"] == "uvit_t2i":
+        out["context"] = torch.randn(B, n["num_clip_token"], n["clip_dim"], generator=g)
+        out["mask_token"] = torch.randn(B, n["num_panoptic_class"], H, Wd, generator=g)
+    return out
+
+
+def _sd_checksum(sd):
+    return np.array([float(v.double().sum()) for v in sd.values()] +
+                    [float(v.double().abs().sum()) for v in sd.values()], dtype=np.float64)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def gen_forward(mods, out):
+    uvit, uvit_t2i = mods[0], mods[1]
+    for name in ["tiny_uvit_cond", "tiny_uvit_h", "tiny_uvit_uncond"]:
+        cfg = C.nnet_kwargs(name)
+        sd = W.nnet_state_dict(cfg, seed=11, init="random")
+        kw = dict(cfg)
+        kw.pop("name")
+        net = uvit.UViT(**kw)
+        net.load_state_dict(sd)
+        net.eval()
+        inp = _inputs(name, 2, seed=5)
+        with torch.no_grad():
+            eps = net(inp["x"], inp["t"], inp.get("y"))
+        out[f"{name}/sd_checksum"] = _sd_checksum(sd)
+        for k, v in inp.items():
+            out[f"{name}/in_{k}"] = _np(v)
+        out[f"{name}/eps"] = _np(eps)
+
+    name = "tiny_t2i"
+    cfg = C.nnet_kwargs(name)
+    sd = W.nnet_state_dict(cfg, seed=11, init="random")
+    kw = dict(cfg)
+    kw.pop("name")
+    net = uvit_t2i.UViT(**kw)
+    net.load_state_dict(sd)
+    net.eval()
+    inp = _inputs(name, 2, seed=5)
+    with torch.no_grad():
+        eps_m, pm = net(inp["x"], inp["t"], inp["context"], mask_token=inp["mask_token"])
+        eps_n = net(inp["x"], inp["t"], inp["context"])
+        eps_g, pm_g = net(inp["x"], inp["t"], inp["context"], mask_token=inp["mask_token"], use_ground_truth=True)
+    out[f"{name}/sd_checksum"] = _sd_checksum(sd)
+    for k, v in inp.items():
+        out[f"{name}/in_{k}"] = _np(v)
+    out[f"{name}/eps_mask"] = _np(eps_m)
+    out[f"{name}/pred_mask"] = _np(pm)
+    out[f"{name}/eps_nomask"] = _np(eps_n)
+    out[f"{name}/eps_gt"] = _np(eps_g)
+
+
+def gen_ops(mods, out):
+    uvit = mods[0]
+    g = torch.Generator().manual_seed(3)
+    t = torch.rand(6, generator=g) * 999.0
+    out["ops/temb_t"] = _np(t)
+    for dim in (64, 144, 1024, 1152, 7):
+        out[f"ops/temb_{dim}"] = _np(uvit.timestep_embedding(t, dim))
+    for p, Cc in ((2, 4), (4, 4), (2, 8)):
+        x = torch.randn(2, 16, p * p * Cc, generator=g)
+        out[f"ops/unpatch_in_{p}_{Cc}"] = _np(x)
+        out[f"ops/unpatch_out_{p}_{Cc}"] = _np(uvit.unpatchify(x, Cc))
+    # attention at the reference's awkward lengths: sampled output elements (inputs regenerated in tests)
+    for L in (257, 258, 334, 590):
+        for Dh in (64, 72):
+            heads = 2
+            D = heads * Dh
+            gg = torch.Generator().manual_seed(1000 + L * 100 + Dh)
+            x = torch.randn(1, L, D, generator=gg)
+            attn = uvit.Attention(D, num_heads=heads)
+            sd = {"qkv.weight": torch.randn(3 * D, D, generator=gg) * D ** -0.5,
+                  "proj.weight": torch.randn(D, D, generator=gg) * D ** -0.5,
+                  "proj.bias": torch.randn(D, generator=gg) * 0.1}
+            attn.load_state_dict(sd)
+            with torch.no_grad():
+                o = attn(x)
+            out[f"ops/attn_{L}_{Dh}"] = _np(o[0, ::7, :])
+
+
+def gen_solver(mods, out):
+    _, _, _, pp, dpt, sde = mods
+    betas = (torch.linspace(0.00085 ** 0.5, 0.0120 ** 0.5, 1000, dtype=torch.float64) ** 2).numpy()
+    out["solver/betas"] = betas
+    ns = pp.NoiseScheduleVP(schedule="discrete", betas=torch.tensor(betas).float())
+    tg = torch.linspace(1.0, 1e-3, 51)
+    out["solver/pp_grid_t"] = _np(tg)
+    out["solver/pp_log_mean"] = _np(ns.marginal_log_mean_coeff(tg))
+    out["solver/pp_std"] = _np(ns.marginal_std(tg))
+    out["solver/pp_lambda"] = _np(ns.marginal_lambda(tg))
+    lam = torch.linspace(-8.0, 7.0, 33)
+    out["solver/pp_inv_lambda_in"] = _np(lam)
+    out["solver/pp_inv_lambda"] = _np(ns.inverse_lambda(lam))
+    nl = dpt.NoiseScheduleVP("linear")
+    tl = torch.linspace(1e-4, 1.0, 37)
+    out["solver/lin_t"] = _np(tl)
+    out["solver/lin_log_mean"] = _np(nl.marginal_log_mean_coeff(tl))
+    out["solver/lin_lambda"] = _np(nl.marginal_lambda(tl))
+    out["solver/lin_inv_lambda"] = _np(nl.inverse_lambda(nl.marginal_lambda(tl)))
+
+    # analytic stand-in models: record every (t) the solver asks for, and the final x / trace
+    g = torch.Generator().manual_seed(9)
+    x0 = torch.randn(2, 4, 8, 8, generator=g)
+    m0 = torch.randn(2, 8, 8, 8, generator=g)
+    out["solver/x_init"] = _np(x0)
+    out["solver/mask_init"] = _np(m0)
+
+    def eps_fn(x, t):
+        return torch.tanh(x) * (0.3 + 0.5 * t.reshape(-1, 1, 1, 1)) + 0.1 * torch.roll(x, 1, dims=-1)
+
+    def mask_fn(m, t):
+        return torch.tanh(0.7 * m + t.reshape(-1, 1, 1, 1))
+
+    # (A) pp, no mask, NFE / times recorded
+    calls = []
+
+    def model_a(x, t_continuous, panoptic=None, mask_token=None, use_ground_truth=False, enable_panoptic=False):
+        calls.append(_np(t_continuous))
+        return eps_fn(x, t_continuous), None
+    solver = pp.DPM_Solver(model_a, ns, predict_x0=True, thresholding=False)
+    xa, _ = solver.sample(x0.clone(), steps=50, eps=1.0 / 1000, T=1.0)
+    out["solver/pp_final"] = _np(xa)
+    out["solver/pp_calls_t"] = np.stack(calls)
+
+    # (A') pp with panoptic mask co-update (enable_mask_opt=True, train_t2i_discrete.py:544)
+    calls = []
+
+    def model_m(x, t_continuous, panoptic=None, mask_token=None, use_ground_truth=False, enable_panoptic=False):
+        calls.append(_np(t_continuous))
+        return eps_fn(x, t_continuous) + 0.05 * mask_token[:, :4], mask_fn(mask_token, t_continuous)
+    solver = pp.DPM_Solver(model_m, ns, predict_x0=True, thresholding=False)
+    xm, pm = solver.sample(x0.clone(), steps=50, eps=1.0 / 1000, T=1.0, order=3, mask_token=m0.clone(),
+                           enable_mask_opt=True, enable_panoptic=True)
+    out["solver/ppm_final"] = _np(xm)
+    out["solver/ppm_pred_mask"] = _np(pm)
+    out["solver/ppm_calls_t"] = np.stack(calls)
+    # and with enable_mask_opt=False (mask state := pred_mask)
+    solver = pp.DPM_Solver(model_m, ns, predict_x0=True, thresholding=False)
+    xm2, pm2 = solver.sample(x0.clone(), steps=50, eps=1.0 / 1000, T=1.0, order=3, mask_token=m0.clone(),
+                             enable_mask_opt=False, enable_panoptic=True)
+    out["solver/ppm_noopt_final"] = _np(xm2)
+    out["solver/ppm_noopt_pred_mask"] = _np(pm2)
+
+    # (B) dpm_solver_pytorch with sde.ScoreModel.noise_pred (t * 999) through model_wrapper('0')
+    calls = []
+
+    def nnet_b(x, t):
+        calls.append(_np(t))
+        return eps_fn(x, t / 999.0)
+    score = sde.ScoreModel(nnet_b, pred="noise_pred", sde=sde.VPSDE())
+    mf = dpt.model_wrapper(score.noise_pred, dpt.NoiseScheduleVP("linear"), time_input_type="0", model_kwargs={})
+    xb = dpt.DPM_Solver(mf, dpt.NoiseScheduleVP("linear")).sample(x0.clone(), steps=50, eps=1e-4,
+                                                                  adaptive_step_size=False, fast_version=True)
+    out["solver/pt_final"] = _np(xb)
+    out["solver/pt_calls_t999"] = np.stack(calls)
+    for steps in (10, 12, 20, 21):  # other step counts (orders tails [2,1] / [1])
+        xs, _ = pp.DPM_Solver(model_a, ns, predict_x0=True).sample(x0.clone(), steps=steps, eps=1e-3, T=1.0)
+        out[f"solver/pp_final_steps{steps}"] = _np(xs)
+        xs = dpt.DPM_Solver(mf, dpt.NoiseScheduleVP("linear")).sample(x0.clone(), steps=steps, eps=1e-4)
+        out[f"solver/pt_final_steps{steps}"] = _np(xs)
+
+
+def gen_sample_tiny(mods, out):
+    """Full 50-NFE CFG samples of tiny nets with both front-ends (reference nets + reference solvers)."""
+    uvit, uvit_t2i, _, pp, dpt, sde = mods
+    betas = (torch.linspace(0.00085 ** 0.5, 0.0120 ** 0.5, 1000, dtype=torch.float64) ** 2).numpy()
+
+    # front-end B on tiny_uvit_cond: eval_ldm.py:66-108
+    name = "tiny_uvit_cond"
+    cfg = C.nnet_kwargs(name)
+    sd = W.nnet_state_dict(cfg, seed=11, init="random")
+    kw = dict(cfg)
+    kw.pop("name")
+    net = uvit.UViT(**kw)
+    net.load_state_dict(sd)
+    net.eval()
+    inp = _inputs(name, 2, seed=21)
+    null = cfg["num_classes"] - 1
+    scale = C.get_config(name)["cfg_scale"]
+
+    def cfg_nnet(x, timesteps, y):
+        c = net(x, timesteps, y=y)
+        u = net(x, timesteps, y=torch.tensor([null] * x.size(0)))
+        return c + scale * (c - u)
+    score = sde.ScoreModel(cfg_nnet, pred="noise_pred", sde=sde.VPSDE())
+    ns = dpt.NoiseScheduleVP(schedule="linear")
+    mf = dpt.model_wrapper(score.noise_pred, ns, time_input_type="0", model_kwargs=dict(y=inp["y"]))
+    with torch.no_grad():
+        z = dpt.DPM_Solver(mf, ns).sample(inp["x"].clone(), steps=50, eps=1e-4, adaptive_step_size=False,
+                                          fast_version=True)
+    out[f"sample/{name}/z_init"] = _np(inp["x"])
+    out[f"sample/{name}/y"] = _np(inp["y"])
+    out[f"sample/{name}/z"] = _np(z)
+
+    # front-end A on tiny_uvit_h: eval_ldm_discrete.py:72-102 semantics (model_fn gets the pp kwargs)
+    name = "tiny_uvit_h"
+    cfg = C.nnet_kwargs(name)
+    sd = W.nnet_state_dict(cfg, seed=11, init="random")
+    kw = dict(cfg)
+    kw.pop("name")
+    net_h = uvit.UViT(**kw)
+    net_h.load_state_dict(sd)
+    net_h.eval()
+    inp = _inputs(name, 2, seed=21)
+    null = cfg["num_classes"] - 1
+    scale = C.get_config(name)["cfg_scale"]
+    nsd = pp.NoiseScheduleVP(schedule="discrete", betas=torch.tensor(betas).float())
+
+    def model_fn(x, t_continuous, panoptic=None, mask_token=None, use_ground_truth=False, enable_panoptic=False):
+        t = t_continuous * 1000
+        c = net_h(x, t, y=inp["y"])
+        u = net_h(x, t, y=torch.tensor([null] * x.size(0)))
+        return c + scale * (c - u), None
+    with torch.no_grad():
+        z, _ = pp.DPM_Solver(model_fn, nsd, predict_x0=True, thresholding=False).sample(
+            inp["x"].clone(), steps=50, eps=1.0 / 1000, T=1.0)
+    out[f"sample/{name}/z_init"] = _np(inp["x"])
+    out[f"sample/{name}/y"] = _np(inp["y"])
+    out[f"sample/{name}/z"] = _np(z)
+
+    # panoptic t2i on tiny_t2i: train_t2i_discrete.py:387-439,480-546
+    name = "tiny_t2i"
+    cfg = C.nnet_kwargs(name)
+    sd = W.nnet_state_dict(cfg, seed=11, init="random")
+    kw = dict(cfg)
+    kw.pop("name")
+    net_t = uvit_t2i.UViT(**kw)
+    net_t.load_state_dict(sd)
+    net_t.eval()
+    inp = _inputs(name, 2, seed=21)
+    g = torch.Generator().manual_seed(77)
+    empty = torch.randn(cfg["num_clip_token"], cfg["clip_dim"], generator=g)
+    scale = C.get_config(name)["cfg_scale"]
+
+    def cfg_t2i(x, timesteps, context, mask_token=None, mask_0=None, use_ground_truth=False, enable_panoptic=False):
+        c, pm = net_t(x, timesteps, context=context, mask_token=mask_token, mask_0=mask_0,
+                      use_ground_truth=use_ground_truth, enable_panoptic=enable_panoptic)
+        ec = empty.unsqueeze(0).expand(x.size(0), -1, -1)
+        u, pmu = net_t(x, timesteps, context=ec, mask_token=mask_token, mask_0=mask_0,
+                       use_ground_truth=use_ground_truth, enable_panoptic=enable_panoptic)
+        pm = pm + scale * (pm - pmu)
+        return c + scale * (c - u), pm
+
+    def model_fn_t(x, t_continuous, panoptic=None, mask_token=None, use_ground_truth=False, enable_panoptic=False):
+        t = t_continuous * 1000
+        return cfg_t2i(x, t, inp["context"], mask_token=mask_token, mask_0=panoptic,
+                       use_ground_truth=use_ground_truth, enable_panoptic=enable_panoptic)
+    with torch.no_grad():
+        z, pm = pp.DPM_Solver(model_fn_t, nsd, predict_x0=True, thresholding=False).sample(
+            inp["x"].clone(), steps=50, eps=1.0 / 1000, T=1.0, order=3, mask_token=inp["mask_token"].clone(),
+            enable_mask_opt=True, use_ground_truth=False, enable_panoptic=True)
+    out[f"sample/{name}/z_init"] = _np(inp["x"])
+    out[f"sample/{name}/context"] = _np(inp["context"])
+    out[f"sample/{name}/empty_context"] = _np(empty)
+    out[f"sample/{name}/mask_init"] = _np(inp["mask_token"])
+    out[f"sample/{name}/z"] = _np(z)
+    out[f"sample/{name}/pred_mask"] = _np(pm)
+
+
+def gen_decoder(mods, out):
+    ae = mods[2]
+    ddc = dict(double_z=True, z_channels=4, resolution=32, in_channels=3, out_ch=3, ch=32, ch_mult=[1, 2],
+               num_res_blocks=1, attn_resolutions=[], dropout=0.0)
+    dec = ae.Decoder(**ddc)
+    sd = W.make_state_dict(W.decoder_spec(ch=32, ch_mult=(1, 2), num_res_blocks=1, prefix="decoder"),
+                           seed=13, init="random")
+    dsd = {k[len("decoder."):]: v for k, v in sd.items() if k.startswith("decoder.")}
+    dec.load_state_dict(dsd)
+    dec.eval()
+    pq = torch.nn.Conv2d(4, 4, 1)
+    pq.load_state_dict({"weight": sd["post_quant_conv.weight"], "bias": sd["post_quant_conv.bias"]})
+    g = torch.Generator().manual_seed(17)
+    z = torch.randn(2, 4, 8, 8, generator=g)
+    with torch.no_grad():
+        img = dec(pq(z / 0.18215))  # FrozenAutoencoderKL.decode, libs/autoencoder.py:446-450
+    out["decoder/sd_checksum"] = _sd_checksum(sd)
+    out["decoder/z"] = _np(z)
+    out["decoder/img"] = _np(img)
+
+
+def gen_utils(ref, out):
+    f = _ref_funcs(os.path.join(ref, "utils.py"), ["int2bits", "bits2int", "amortize"])
+    g = torch.Generator().manual_seed(23)
+    ids = torch.randint(0, 256, (2, 1, 8, 8), generator=g)
+    ids[0, 0, 0, :4] = torch.tensor([0, 1, 128, 255])
+    bits = f["int2bits"](ids, out_dtype=torch.float)
+    back = f["bits2int"](bits > 0)
+    out["utils/ids"] = _np(ids)
+    out["utils/bits"] = _np(bits)
+    out["utils/bits2int"] = _np(back)
+    out["utils/amortize"] = np.array(f["amortize"](103, 25) + [-1] + f["amortize"](100, 25))
+
+
+def main():
+    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    mods = _import_reference(ref)
+    torch.set_num_threads(8)
+    out = {}
+    gen_forward(mods, out)
+    gen_ops(mods, out)
+    gen_solver(mods, out)
+    gen_sample_tiny(mods, out)
+    gen_decoder(mods, out)
+    gen_utils(ref, out)
+    path = os.path.join(HERE, "golden.npz")
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in out.items()})
+    print(f"wrote {path}: {len(out)} arrays, {os.path.getsize(path) / 1e6:.2f} MB")
+
+
+if __name__ == "__main__":
+    main()
