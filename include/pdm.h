@@ -1,0 +1,127 @@
+/* libpdm — MI355X (gfx950) HIP implementation of the Panoptic-Diffusion sampling hot path.
+ *
+ * C ABI only: plain pointers, sizes and a hipStream_t (passed as void*).  All device buffers are owned
+ * by the caller (torch tensors on the Python side); a pdm_uvit handle stores configuration and the
+ * device addresses of the caller-owned packed weights, nothing else.  Every entry point is
+ * stream-ordered and asynchronous; it returns 0 on success or a non-zero status, with the message in
+ * pdm_last_error() (thread-local).  No entry point allocates, frees or synchronises, so all of them can
+ * be captured into a HIP graph.
+ *
+ * The reference has no FFI: its boundary is Python.  Each entry point below names
+ * the reference call it replaces; the Python package panopticdiffusionmodels_amd keeps the reference
+ * signatures above it (get_nnet / nnet(...) / NoiseScheduleVP / DPM_Solver.sample / decode).
+ */
+#ifndef PDM_H
+#define PDM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PDM_OK 0
+#define PDM_ERR_ARG 1     /* invalid argument / unsupported shape (Python: ValueError) */
+#define PDM_ERR_HIP 2     /* HIP runtime error (Python: RuntimeError) */
+#define PDM_ERR_STATE 3   /* missing weight / not prepared (Python: RuntimeError) */
+
+#define PDM_F32 0
+#define PDM_BF16 1
+
+/* GEMM epilogues */
+#define PDM_EPI_BF16 0   /* out_bf16 = A W^T + b */
+#define PDM_EPI_GELU 1   /* out_bf16 = gelu_erf(A W^T + b) */
+#define PDM_EPI_F32 2    /* out_f32 (+)= A W^T + b, optional bf16 copy into out_bf16 */
+
+const char* pdm_last_error(void);
+int pdm_version(void);
+int pdm_device_arch(char* buf, int len);   /* gcnArchName of the current device, e.g. "gfx950:sramecc+:xnack-" */
+
+/* ---- network handle: libs/uvit.py:138-230 UViT, libs/uvit_t2i.py:258-525 UViT (t2i) -------------- */
+typedef struct pdm_uvit pdm_uvit;
+
+typedef struct pdm_uvit_cfg {
+  int img_size, patch_size, in_chans, embed_dim, depth, num_heads;
+  int mlp_hidden;          /* int(embed_dim * mlp_ratio) */
+  int num_classes;         /* <= 0: unconditional (no label token) */
+  int conv;                /* final 3x3 conv present (applied by pdm_stage_epilogue, not by forward) */
+  int skip;                /* long skips present */
+  int qkv_bias;
+  int mlp_time_embed;      /* must be 0 (all reference configs) */
+  /* t2i (libs/uvit_t2i.py) */
+  int t2i;
+  int clip_dim, num_clip_token;
+  int separate, enable_panoptic, num_panoptic_class;
+} pdm_uvit_cfg;
+
+/* replaces utils.get_nnet (utils.py:291-299) + UViT.__init__ (libs/uvit.py:139-195) */
+int pdm_uvit_create(const pdm_uvit_cfg* cfg, pdm_uvit** out);
+int pdm_uvit_destroy(pdm_uvit* h);
+/* replaces load_state_dict (eval_ldm_discrete.py:46): register the device address of one packed weight
+ * under its reference state_dict key.  Linear weights bf16 [out, in]; everything
+ * else fp32.  decoder_pred(.mask).weight is bf16 padded to a multiple of 16 rows. */
+int pdm_uvit_set_param(pdm_uvit* h, const char* name, const void* dev_ptr, int dtype, long long numel);
+/* enumerate the keys the handle expects (name, dtype, element count) */
+int pdm_uvit_param_count(const pdm_uvit* h);
+int pdm_uvit_param_info(const pdm_uvit* h, int i, char* name, int len, int* dtype, long long* numel);
+/* checks every required key is registered with the expected dtype / size */
+int pdm_uvit_validate(pdm_uvit* h);
+int pdm_uvit_workspace_size(const pdm_uvit* h, int rows, size_t* bytes);
+
+/* replaces UViT.forward (libs/uvit.py:201-230) up to and including unpatchify: writes the pre-final-conv
+ * output eps_pre [rows, C, H, W] fp32.  x [rows, C, H, W] fp32, t [rows] fp32 (as the net receives it),
+ * y [rows] int64 or NULL.  The final conv (if any) + CFG are applied by pdm_stage_epilogue. */
+int pdm_uvit_forward(pdm_uvit* h, const float* x, const float* t, const int64_t* y, float* eps_pre, int rows,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* replaces UViT(t2i).forward (libs/uvit_t2i.py:378-525).  context [rows, num_clip_token, clip_dim] fp32,
+ * mask_token [rows, K, H, W] fp32 or NULL.  Writes eps_pre [rows, C, H, W] and (if mask_token and not
+ * use_ground_truth) mask_pre [rows, K, H, W] (pre-final-conv, pre-tanh). */
+int pdm_uvit_t2i_forward(pdm_uvit* h, const float* x, const float* t, const float* context,
+                         const float* mask_token, int use_ground_truth, float* eps_pre, float* mask_pre,
+                         int rows, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- solver / guidance epilogue ------------------------------------------------------------------
+ * final_layer conv3x3 (libs/uvit.py:183,229) + CFG combine (eval_ldm_discrete.py:77, eval_ldm.py:71,
+ * train_t2i_discrete.py:429-431) + optional tanh (libs/uvit_t2i.py:513) + the DPM-Solver stage
+ * arithmetic (dpm_solver_pp.py:310-328 x0 conversion, 420-829 linear combinations).  Per element:
+ *   act(v) = tanh(v) if act_tanh else v   (per call, before the combine: libs/uvit_t2i.py:513 then 429)
+ *   e = act(conv(pre[b])) (conv skipped if conv_w == NULL)
+ *   if has_uncond: e += cfg_scale * (e - act(conv(pre[b+B])))
+ *   m = ax * xin + ae * e   (xin may be NULL -> m = ae * e);   m_out = m (if not NULL)
+ *   x_out = cm * m + sum_i c[i] * T[i]   (if not NULL)                                            */
+typedef struct pdm_stage_epilogue_args {
+  const float* pre;
+  const float* conv_w; const float* conv_b;
+  int B, C, H, W;
+  int has_uncond; float cfg_scale;
+  int act_tanh;
+  const float* xin; float ax, ae;
+  float* m_out;
+  int n_terms; const float* T[6]; float c[6]; float cm;
+  float* x_out;
+} pdm_stage_epilogue_args;
+int pdm_stage_epilogue(const pdm_stage_epilogue_args* a, void* stream);
+
+/* out = sum_i c[i] * T[i], n fp32 elements (generic DPM_Solver update path, dpm_solver_pytorch.py:301-432) */
+int pdm_lincomb(float* out, int n_terms, const float* const* T, const float* c, long long n, void* stream);
+
+/* ---- individual kernels (exposed for parity tests and the generic Python path) -------------------- */
+/* nn.Linear on bf16 rows: libs/uvit.py:61-63,117; libs/timm.py:101-104.  W [N][K] bf16. */
+int pdm_gemm_bf16(const void* A1, int lda1, const void* A2, int lda2, int K1, const void* W, const float* bias,
+                  int M, int N, int K, int epi, void* out_bf16, int ldo, float* out_f32, int ldr, int accumulate,
+                  void* stream);
+/* nn.LayerNorm (libs/uvit.py:100,103,180): fp32 rows -> bf16 rows */
+int pdm_layernorm(const float* x, int ldx, const float* gamma, const float* beta, void* y, int ldy, int rows, int D,
+                  float eps, void* stream);
+/* Attention core (libs/uvit.py:66-92 minus the two Linears): packed qkv bf16 -> bf16 */
+int pdm_attention(const void* qkv, int ldq, void* out, int ldo, int B, int L, int H, int Dh, float scale,
+                  void* stream);
+/* fp32 -> bf16 conversion */
+int pdm_f32_to_bf16(const float* x, void* y, long long n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PDM_H */

@@ -1,0 +1,200 @@
+"""ctypes binding of libpdm.so (include/pdm.h).
+
+The product path has no fallback: if the HIP library is missing, cannot be loaded, or no GPU is
+present, calls raise.  Status codes map to the exception types of the reference (ValueError for bad
+arguments / unsupported shapes, RuntimeError otherwise).
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpdm.so")
+
+PDM_F32, PDM_BF16 = 0, 1
+EPI_BF16, EPI_GELU, EPI_F32 = 0, 1, 2
+
+
+class PdmUvitCfg(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "img_size", "patch_size", "in_chans", "embed_dim", "depth", "num_heads", "mlp_hidden", "num_classes",
+        "conv", "skip", "qkv_bias", "mlp_time_embed", "t2i", "clip_dim", "num_clip_token", "separate",
+        "enable_panoptic", "num_panoptic_class")]
+
+
+class PdmStageEpilogueArgs(ctypes.Structure):
+    _fields_ = [
+        ("pre", ctypes.c_void_p), ("conv_w", ctypes.c_void_p), ("conv_b", ctypes.c_void_p),
+        ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("has_uncond", ctypes.c_int), ("cfg_scale", ctypes.c_float), ("act_tanh", ctypes.c_int),
+        ("xin", ctypes.c_void_p), ("ax", ctypes.c_float), ("ae", ctypes.c_float),
+        ("m_out", ctypes.c_void_p),
+        ("n_terms", ctypes.c_int), ("T", ctypes.c_void_p * 6), ("c", ctypes.c_float * 6), ("cm", ctypes.c_float),
+        ("x_out", ctypes.c_void_p),
+    ]
+
+
+_SIGS = {
+    "pdm_last_error": (ctypes.c_char_p, []),
+    "pdm_version": (ctypes.c_int, []),
+    "pdm_device_arch": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    "pdm_uvit_create": (ctypes.c_int, [ctypes.POINTER(PdmUvitCfg), ctypes.POINTER(ctypes.c_void_p)]),
+    "pdm_uvit_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "pdm_uvit_set_param": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int,
+                                          ctypes.c_longlong]),
+    "pdm_uvit_param_count": (ctypes.c_int, [ctypes.c_void_p]),
+    "pdm_uvit_param_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_longlong)]),
+    "pdm_uvit_validate": (ctypes.c_int, [ctypes.c_void_p]),
+    "pdm_uvit_workspace_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
+    "pdm_uvit_forward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.c_void_p]),
+    "pdm_uvit_t2i_forward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "pdm_stage_epilogue": (ctypes.c_int, [ctypes.POINTER(PdmStageEpilogueArgs), ctypes.c_void_p]),
+    "pdm_lincomb": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                   ctypes.POINTER(ctypes.c_float), ctypes.c_longlong, ctypes.c_void_p]),
+    "pdm_gemm_bf16": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_void_p]),
+    "pdm_layernorm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                     ctypes.c_void_p]),
+    "pdm_attention": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p]),
+    "pdm_f32_to_bf16": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+def load():
+    """Load libpdm.so (no GPU needed to load; every compute call needs one)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libpdm.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; "
+                           f"g.build()'` (or `make -C panopticdiffusionmodels_amd/csrc`)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status, what=""):
+    if status != 0:
+        msg = load().pdm_last_error().decode()
+        if status == 1:
+            raise ValueError(f"{what}: {msg}" if what else msg)
+        raise RuntimeError(f"{what}: {msg}" if what else msg)
+
+
+def require_gpu(t=None):
+    if not torch.cuda.is_available():
+        raise RuntimeError("panopticdiffusionmodels_amd runs on an MI355X (gfx950) GPU; no GPU is visible "
+                           "(there is no CPU fallback in the product path)")
+    if t is not None and t.device.type != "cuda":
+        raise RuntimeError(f"expected a tensor on the GPU, got device {t.device}")
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+# ---- thin op wrappers (used by tests and the generic solver path) ----------------------------------
+
+def gemm(a, w, bias=None, epi=EPI_BF16, out=None, out_f32=None, accumulate=False, a2=None):
+    """C = [a | a2] @ w.T (+ bias) with the selected epilogue.  a/a2/w bf16 2-D contiguous rows."""
+    lib = load()
+    require_gpu(a)
+    M, K1 = a.shape
+    K = K1 + (a2.shape[1] if a2 is not None else 0)
+    N = w.shape[0]
+    assert w.shape[1] == K
+    if epi in (EPI_BF16, EPI_GELU) and out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    if epi == EPI_F32 and out_f32 is None:
+        out_f32 = torch.zeros(M, N, dtype=torch.float32, device=a.device)
+    check(lib.pdm_gemm_bf16(ptr(a), a.stride(0), ptr(a2), a2.stride(0) if a2 is not None else 0, K1, ptr(w),
+                            ptr(bias), M, N, K, epi, ptr(out), out.stride(0) if out is not None else 0,
+                            ptr(out_f32), out_f32.stride(0) if out_f32 is not None else 0, int(accumulate),
+                            stream_ptr(a.device)), "pdm_gemm_bf16")
+    return out_f32 if epi == EPI_F32 else out
+
+
+def layernorm(x, gamma, beta, eps=1e-5):
+    lib = load()
+    require_gpu(x)
+    rows, D = x.shape
+    y = torch.empty(rows, D, dtype=torch.bfloat16, device=x.device)
+    check(lib.pdm_layernorm(ptr(x), x.stride(0), ptr(gamma), ptr(beta), ptr(y), y.stride(0), rows, D, eps,
+                            stream_ptr(x.device)), "pdm_layernorm")
+    return y
+
+
+def attention(qkv, B, L, H, Dh, scale=None):
+    lib = load()
+    require_gpu(qkv)
+    out = torch.empty(B * L, H * Dh, dtype=torch.bfloat16, device=qkv.device)
+    scale = Dh ** -0.5 if scale is None else scale
+    check(lib.pdm_attention(ptr(qkv), qkv.stride(0), ptr(out), out.stride(0), B, L, H, Dh, scale,
+                            stream_ptr(qkv.device)), "pdm_attention")
+    return out
+
+
+def lincomb(terms, coeffs, out=None):
+    """out = sum_i coeffs[i] * terms[i] (fp32, same shape, contiguous)."""
+    lib = load()
+    t0 = terms[0]
+    require_gpu(t0)
+    n = len(terms)
+    if n > 8:
+        raise ValueError("lincomb supports at most 8 terms")
+    if out is None:
+        out = torch.empty_like(t0)
+    arr = (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t in terms])
+    cs = (ctypes.c_float * max(n, 1))(*[float(c) for c in coeffs])
+    check(lib.pdm_lincomb(ptr(out), n, arr, cs, t0.numel(), stream_ptr(t0.device)), "pdm_lincomb")
+    return out
+
+
+def stage_epilogue(pre, B, conv_w=None, conv_b=None, cfg_scale=None, act_tanh=False, xin=None, ax=0.0, ae=1.0,
+                   m_out=None, terms=(), coeffs=(), cm=0.0, x_out=None):
+    """See pdm_stage_epilogue in include/pdm.h.  pre [B or 2B, C, H, W] fp32 contiguous."""
+    lib = load()
+    require_gpu(pre)
+    _, C, H, W = pre.shape
+    a = PdmStageEpilogueArgs()
+    a.pre = pre.data_ptr()
+    a.conv_w = conv_w.data_ptr() if conv_w is not None else None
+    a.conv_b = conv_b.data_ptr() if conv_b is not None else None
+    a.B, a.C, a.H, a.W = B, C, H, W
+    a.has_uncond = int(cfg_scale is not None)
+    a.cfg_scale = float(cfg_scale or 0.0)
+    a.act_tanh = int(act_tanh)
+    a.xin = xin.data_ptr() if xin is not None else None
+    a.ax, a.ae = float(ax), float(ae)
+    a.m_out = m_out.data_ptr() if m_out is not None else None
+    if len(terms) > 6:
+        raise ValueError("stage_epilogue supports at most 6 terms")
+    a.n_terms = len(terms)
+    for i, (t, c) in enumerate(zip(terms, coeffs)):
+        a.T[i] = t.data_ptr()
+        a.c[i] = float(c)
+    a.cm = float(cm)
+    a.x_out = x_out.data_ptr() if x_out is not None else None
+    check(lib.pdm_stage_epilogue(ctypes.byref(a), stream_ptr(pre.device)), "pdm_stage_epilogue")

@@ -56,8 +56,8 @@ CONFIGS = {
         sample_steps=50, eps=1e-4, mini_batch_size=2,
     ),
     "tiny_uvit_h": dict(  # Dh = 72 (U-ViT-H head dim), patch 4, no conv
-        nnet=dict(name="uvit", img_size=32, patch_size=4, in_chans=4, embed_dim=144, depth=2,
-                  num_heads=2, mlp_ratio=4, qkv_bias=False, mlp_time_embed=False, num_classes=11,
+        nnet=dict(name="uvit", img_size=32, patch_size=4, in_chans=4, embed_dim=576, depth=2,
+                  num_heads=8, mlp_ratio=4, qkv_bias=False, mlp_time_embed=False, num_classes=11,
                   conv=False),
         z_shape=(4, 32, 32), front_end="dpm_solver_pp", cfg_scale=0.7, decode=False,
         sample_steps=50, mini_batch_size=2,
@@ -70,7 +70,7 @@ CONFIGS = {
     ),
     "tiny_t2i": dict(  # panoptic co-generation, separate streams
         nnet=dict(name="uvit_t2i", img_size=16, in_chans=4, patch_size=2, embed_dim=64, depth=2,
-                  num_heads=2, mlp_ratio=4, qkv_bias=False, mlp_time_embed=False, clip_dim=48,
+                  num_heads=2, mlp_ratio=4, qkv_bias=False, mlp_time_embed=False, clip_dim=64,
                   num_clip_token=5, enable_panoptic=True, use_ground_truth=False, separate=True,
                   num_panoptic_class=8),
         z_shape=(4, 16, 16), front_end="dpm_solver_pp", cfg_scale=1.0, decode=False,

@@ -1,0 +1,495 @@
+// C ABI of libpdm (include/pdm.h) and the U-ViT forward drivers.
+//
+// The drivers restate the layer loops of libs/uvit.py:201-230 and libs/uvit_t2i.py:378-525 as a fixed
+// sequence of stream-ordered kernel launches over a caller-owned workspace: no allocation, no host sync,
+// so a whole forward (or a whole sampler step) can be captured into a HIP graph.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/pdm.h"
+#include "pdm_kernels.h"
+
+using pdm::bf16;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define PDM_HIP(call)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess) return fail(PDM_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define PDM_CHECK(msg_expr)                          \
+  do {                                               \
+    const char* m_ = (msg_expr);                     \
+    if (m_) return fail(PDM_ERR_ARG, m_);            \
+  } while (0)
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct ParamSpec {
+  int dtype;
+  long long numel;
+  const void* ptr = nullptr;
+};
+
+}  // namespace
+
+struct pdm_uvit {
+  pdm_uvit_cfg cfg;
+  int D, H, Dh, Hid, C, p, n_patch, extras, Lx, Lm, P, P_pad, K, PK, PK_pad, depth, nhalf;
+  std::vector<std::string> order;
+  std::map<std::string, ParamSpec> params;
+
+  void add(const std::string& name, int dtype, long long numel) {
+    order.push_back(name);
+    params[name] = ParamSpec{dtype, numel, nullptr};
+  }
+  const void* ptr(const std::string& name) const {
+    auto it = params.find(name);
+    return it == params.end() ? nullptr : it->second.ptr;
+  }
+  const float* f(const std::string& name) const { return static_cast<const float*>(ptr(name)); }
+  const bf16* w(const std::string& name) const { return static_cast<const bf16*>(ptr(name)); }
+
+  void add_block(const std::string& pre, bool skip) {
+    add(pre + ".norm1.weight", PDM_F32, D);
+    add(pre + ".norm1.bias", PDM_F32, D);
+    add(pre + ".attn.qkv.weight", PDM_BF16, 3LL * D * D);
+    if (cfg.qkv_bias) add(pre + ".attn.qkv.bias", PDM_F32, 3LL * D);
+    add(pre + ".attn.proj.weight", PDM_BF16, 1LL * D * D);
+    add(pre + ".attn.proj.bias", PDM_F32, D);
+    add(pre + ".norm2.weight", PDM_F32, D);
+    add(pre + ".norm2.bias", PDM_F32, D);
+    add(pre + ".mlp.fc1.weight", PDM_BF16, 1LL * Hid * D);
+    add(pre + ".mlp.fc1.bias", PDM_F32, Hid);
+    add(pre + ".mlp.fc2.weight", PDM_BF16, 1LL * D * Hid);
+    add(pre + ".mlp.fc2.bias", PDM_F32, D);
+    if (skip) {
+      add(pre + ".skip_linear.weight", PDM_BF16, 2LL * D * D);
+      add(pre + ".skip_linear.bias", PDM_F32, D);
+    }
+  }
+};
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// workspace layout
+struct Workspace {
+  float* X;     // [rows*Lx, D] residual stream (image)
+  bf16* XB;     // [rows*Lx, D] bf16 copy of x for the next skip_linear
+  bf16* HN;     // [rows*Lmax, D] LayerNorm output
+  bf16* QKV;    // [rows*Lmax, 3D]
+  bf16* ATT;    // [rows*Lmax, D]
+  bf16* MLP;    // [rows*Lmax, Hid]
+  bf16* SK;     // [nhalf][rows*Lx, D] long-skip activations (image)
+  bf16* HEADIN; // [rows*n_patch, D]
+  // t2i
+  float* CTXF;  // [rows*n_ctx, D] embedded context (fp32)
+  bf16* CTXB;   // [rows*n_ctx, clip_dim] bf16 context
+  float* MX;    // [rows*Lm, D] mask stream
+  bf16* MXB;    // [rows*Lm, D] bf16 copy of the mask-stream block output
+  bf16* MXIN;   // [rows*Lm, D] bf16 copy of the mask-stream block input (skip_linear operand)
+  bf16* SKM;    // [nhalf][rows*Lm, D]
+  size_t bytes;
+};
+
+Workspace layout(const pdm_uvit* h, int rows, char* base) {
+  Workspace w{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off = align_up(off + bytes, 256);
+    return p;
+  };
+  const size_t D = h->D;
+  const size_t Mx = (size_t)rows * h->Lx;
+  const bool mask = h->cfg.t2i && h->cfg.separate && h->cfg.enable_panoptic;
+  const size_t Mm = mask ? (size_t)rows * h->Lm : 0;
+  const size_t Mmax = Mx > Mm ? Mx : Mm;
+  w.X = (float*)take(Mx * D * 4);
+  w.XB = (bf16*)take(Mx * D * 2);
+  w.HN = (bf16*)take(Mmax * D * 2);
+  w.QKV = (bf16*)take(Mmax * 3 * D * 2);
+  w.ATT = (bf16*)take(Mmax * D * 2);
+  w.MLP = (bf16*)take(Mmax * h->Hid * 2);
+  w.SK = (bf16*)take((size_t)h->nhalf * Mx * D * 2);
+  w.HEADIN = (bf16*)take((size_t)rows * h->n_patch * D * 2);
+  if (h->cfg.t2i) {
+    w.CTXF = (float*)take((size_t)rows * h->cfg.num_clip_token * D * 4);
+    w.CTXB = (bf16*)take((size_t)rows * h->cfg.num_clip_token * h->cfg.clip_dim * 2);
+  }
+  if (mask) {
+    w.MX = (float*)take(Mm * D * 4);
+    w.MXB = (bf16*)take(Mm * D * 2);
+    w.MXIN = (bf16*)take(Mm * D * 2);
+    w.SKM = (bf16*)take((size_t)h->nhalf * Mm * D * 2);
+  }
+  w.bytes = off;
+  return w;
+}
+
+// ------------------------------------------------------------------------------------------------
+struct Ctx {
+  const pdm_uvit* h;
+  hipStream_t s;
+};
+
+int gemm(const Ctx& c, const bf16* A, int lda, const bf16* W, const float* bias, int M, int N, int K, int epi,
+         bf16* ob, int ldo, float* of, int ldr, int accumulate, const bf16* A2 = nullptr, int lda2 = 0, int K1 = 0,
+         int a_rpg = 0, int a_gs = 0) {
+  pdm::GemmArgs a{};
+  a.A1 = A; a.lda1 = lda;
+  a.A2 = A2; a.lda2 = lda2;
+  a.K1 = A2 ? K1 : K;
+  a.W = W; a.bias = bias;
+  a.M = M; a.N = N; a.K = K;
+  a.out_bf16 = ob; a.ldo = ldo;
+  a.out_f32 = of; a.ldr = ldr;
+  a.accumulate = accumulate;
+  a.a_rows_per_group = a_rpg; a.a_group_stride = a_gs;
+  PDM_CHECK(pdm::gemm_check(a, epi));
+  PDM_HIP(pdm::gemm_launch(a, epi, c.s));
+  return PDM_OK;
+}
+
+int layernorm(const Ctx& c, const float* x, const std::string& pre, bf16* y, int rows, int rpg = 1, int gs = 1,
+              int off = 0) {
+  pdm::LayerNormArgs a{};
+  a.x = x; a.ldx = c.h->D;
+  a.gamma = c.h->f(pre + ".weight"); a.beta = c.h->f(pre + ".bias");
+  a.y = y; a.ldy = c.h->D;
+  a.rows = rows; a.D = c.h->D;
+  a.rows_per_group = rpg; a.group_stride = gs; a.row_offset = off;
+  a.eps = 1e-5f;
+  PDM_CHECK(pdm::layernorm_check(a));
+  PDM_HIP(pdm::layernorm_launch(a, c.s));
+  return PDM_OK;
+}
+
+#define PDM_TRY(x)           \
+  do {                       \
+    int r_ = (x);            \
+    if (r_) return r_;       \
+  } while (0)
+
+// One U-ViT Block (libs/uvit.py:115-120) on `rows_L` token rows of width D held in X (fp32).
+//   skip_in:  bf16 [rows_L, D] skip activation (out-blocks), with xin_bf16 the bf16 copy of X
+//   xb_out:   where fc2's epilogue writes the bf16 copy of the block output (or null)
+int run_block(const Ctx& c, const std::string& pre, float* X, int nseq, int L, const bf16* xin_bf16,
+              const bf16* skip_in, bf16* xb_out, const Workspace& w) {
+  const pdm_uvit* h = c.h;
+  const int D = h->D, M = nseq * L;
+  if (skip_in) {
+    PDM_TRY(gemm(c, xin_bf16, D, h->w(pre + ".skip_linear.weight"), h->f(pre + ".skip_linear.bias"), M, D, 2 * D,
+                 pdm::EPI_F32, nullptr, 0, X, D, 0, skip_in, D, D));
+  }
+  PDM_TRY(layernorm(c, X, pre + ".norm1", w.HN, M));
+  PDM_TRY(gemm(c, w.HN, D, h->w(pre + ".attn.qkv.weight"), h->cfg.qkv_bias ? h->f(pre + ".attn.qkv.bias") : nullptr,
+               M, 3 * D, D, pdm::EPI_BF16, w.QKV, 3 * D, nullptr, 0, 0));
+  {
+    pdm::AttentionArgs a{};
+    a.qkv = w.QKV; a.ldq = 3 * D;
+    a.out = w.ATT; a.ldo = D;
+    a.B = nseq; a.L = L; a.H = h->H; a.Dh = h->Dh;
+    a.scale = 1.0f / sqrtf((float)h->Dh);
+    PDM_CHECK(pdm::attention_check(a));
+    PDM_HIP(pdm::attention_launch(a, c.s));
+  }
+  PDM_TRY(gemm(c, w.ATT, D, h->w(pre + ".attn.proj.weight"), h->f(pre + ".attn.proj.bias"), M, D, D, pdm::EPI_F32,
+               nullptr, 0, X, D, 1));
+  PDM_TRY(layernorm(c, X, pre + ".norm2", w.HN, M));
+  PDM_TRY(gemm(c, w.HN, D, h->w(pre + ".mlp.fc1.weight"), h->f(pre + ".mlp.fc1.bias"), M, h->Hid, D, pdm::EPI_GELU,
+               w.MLP, h->Hid, nullptr, 0, 0));
+  PDM_TRY(gemm(c, w.MLP, h->Hid, h->w(pre + ".mlp.fc2.weight"), h->f(pre + ".mlp.fc2.bias"), M, D, h->Hid,
+               pdm::EPI_F32, xb_out, D, X, D, 1));
+  return PDM_OK;
+}
+
+int check_ready(pdm_uvit* h) {
+  for (auto& n : h->order)
+    if (!h->params[n].ptr) return fail(PDM_ERR_STATE, "pdm_uvit: weight not registered: " + n);
+  return PDM_OK;
+}
+
+int run_head(const Ctx& c, const Workspace& w, int rows, const float* Xsrc, int L_src, int row_off,
+             const std::string& norm, const std::string& head, int Cout, int P, int P_pad, float* out, bool ln) {
+  const pdm_uvit* h = c.h;
+  const int D = h->D;
+  const bf16* hin = w.HEADIN;
+  if (ln) {
+    PDM_TRY(layernorm(c, Xsrc, norm, w.HEADIN, rows * h->n_patch, h->n_patch, L_src, row_off));
+  }
+  pdm::HeadArgs a{};
+  a.x = hin; a.ldx = D;
+  a.W = h->w(head + ".weight"); a.bias = h->f(head + ".bias");
+  a.out = out;
+  a.B = rows; a.D = D; a.C = Cout; a.p = h->p; a.Himg = h->cfg.img_size; a.Wimg = h->cfg.img_size;
+  a.P = P; a.P_pad = P_pad; a.act_tanh = 0;
+  PDM_CHECK(pdm::head_check(a));
+  PDM_HIP(pdm::head_launch(a, c.s));
+  return PDM_OK;
+}
+
+}  // namespace
+
+// ==================================================================================================
+extern "C" {
+
+const char* pdm_last_error(void) { return g_err.c_str(); }
+
+int pdm_version(void) { return 1; }
+
+int pdm_device_arch(char* buf, int len) {
+  int dev = 0;
+  PDM_HIP(hipGetDevice(&dev));
+  hipDeviceProp_t prop;
+  PDM_HIP(hipGetDeviceProperties(&prop, dev));
+  snprintf(buf, len, "%s", prop.gcnArchName);
+  return PDM_OK;
+}
+
+int pdm_uvit_create(const pdm_uvit_cfg* cfg, pdm_uvit** out) {
+  if (!cfg || !out) return fail(PDM_ERR_ARG, "pdm_uvit_create: null argument");
+  const pdm_uvit_cfg& c = *cfg;
+  if (c.embed_dim <= 0 || c.num_heads <= 0 || c.embed_dim % c.num_heads) return fail(PDM_ERR_ARG, "embed_dim must be divisible by num_heads");
+  if (c.patch_size <= 0 || c.img_size % c.patch_size) return fail(PDM_ERR_ARG, "img_size must be divisible by patch_size");
+  if (c.mlp_time_embed) return fail(PDM_ERR_ARG, "mlp_time_embed=True is not supported by the HIP path");
+  if (c.embed_dim % 64) return fail(PDM_ERR_ARG, "embed_dim must be a multiple of 64");
+  if (c.mlp_hidden % 64) return fail(PDM_ERR_ARG, "mlp hidden size must be a multiple of 64");
+  if (c.t2i && c.enable_panoptic && !c.separate)
+    return fail(PDM_ERR_ARG, "uvit_t2i with enable_panoptic and separate=False is not supported by the HIP path");
+  pdm_uvit* h = new pdm_uvit();
+  h->cfg = c;
+  h->D = c.embed_dim;
+  h->H = c.num_heads;
+  h->Dh = c.embed_dim / c.num_heads;
+  h->Hid = c.mlp_hidden;
+  h->C = c.in_chans;
+  h->p = c.patch_size;
+  h->n_patch = (c.img_size / c.patch_size) * (c.img_size / c.patch_size);
+  h->depth = c.depth;
+  h->nhalf = c.depth / 2;
+  h->P = c.patch_size * c.patch_size * c.in_chans;
+  h->P_pad = (h->P + 15) / 16 * 16;
+  h->K = c.num_panoptic_class;
+  h->PK = c.patch_size * c.patch_size * c.num_panoptic_class;
+  h->PK_pad = (h->PK + 15) / 16 * 16;
+  if (h->P_pad > 64 || (c.t2i && c.enable_panoptic && h->PK_pad > 64)) {
+    delete h;
+    return fail(PDM_ERR_ARG, "patch_size^2 * channels must be <= 64");
+  }
+  if (!c.t2i) {
+    h->extras = c.num_classes > 0 ? 2 : 1;
+  } else {
+    h->extras = 1 + c.num_clip_token;
+    if (c.clip_dim % 64) {
+      delete h;
+      return fail(PDM_ERR_ARG, "clip_dim must be a multiple of 64");
+    }
+  }
+  h->Lx = h->extras + h->n_patch;
+  h->Lm = h->Lx + h->n_patch;
+  const int D = h->D;
+  const int pk = c.in_chans * c.patch_size * c.patch_size;
+  h->add("pos_embed", PDM_F32, (long long)h->Lx * D);
+  h->add("patch_embed.proj.weight", PDM_F32, (long long)D * pk);
+  h->add("patch_embed.proj.bias", PDM_F32, D);
+  if (!c.t2i && c.num_classes > 0) h->add("label_emb.weight", PDM_F32, (long long)c.num_classes * D);
+  if (c.t2i) {
+    h->add("context_embed.weight", PDM_BF16, (long long)D * c.clip_dim);
+    h->add("context_embed.bias", PDM_F32, D);
+  }
+  for (int i = 0; i < h->nhalf; ++i) h->add_block("in_blocks." + std::to_string(i), false);
+  h->add_block("mid_block", false);
+  for (int i = 0; i < h->nhalf; ++i) h->add_block("out_blocks." + std::to_string(i), c.skip != 0);
+  h->add("norm.weight", PDM_F32, D);
+  h->add("norm.bias", PDM_F32, D);
+  h->add("decoder_pred.weight", PDM_BF16, (long long)h->P_pad * D);
+  h->add("decoder_pred.bias", PDM_F32, h->P);
+  if (c.t2i && c.enable_panoptic && c.separate) {
+    h->add("pos_embed_mask", PDM_F32, (long long)h->n_patch * D);
+    h->add("mask_embed.proj.weight", PDM_F32, (long long)D * h->PK);
+    h->add("mask_embed.proj.bias", PDM_F32, D);
+    h->add("decoder_pred_mask.weight", PDM_BF16, (long long)h->PK_pad * D);
+    h->add("decoder_pred_mask.bias", PDM_F32, h->PK);
+    for (int i = 0; i < h->nhalf; ++i) h->add_block("in_blocks_mask." + std::to_string(i), false);
+    h->add_block("mid_block_mask", false);
+    for (int i = 0; i < h->nhalf; ++i) h->add_block("out_blocks_mask." + std::to_string(i), c.skip != 0);
+    for (int i = 0; i <= c.depth; ++i) {
+      const std::string zc = "zero_convs." + std::to_string(2 * i + 1) + ".conv";
+      h->add(zc + ".weight", PDM_BF16, (long long)D * D);
+      h->add(zc + ".bias", PDM_F32, D);
+    }
+  }
+  *out = h;
+  return PDM_OK;
+}
+
+int pdm_uvit_destroy(pdm_uvit* h) {
+  delete h;
+  return PDM_OK;
+}
+
+int pdm_uvit_param_count(const pdm_uvit* h) { return h ? (int)h->order.size() : 0; }
+
+int pdm_uvit_param_info(const pdm_uvit* h, int i, char* name, int len, int* dtype, long long* numel) {
+  if (!h || i < 0 || i >= (int)h->order.size()) return fail(PDM_ERR_ARG, "pdm_uvit_param_info: index out of range");
+  const std::string& n = h->order[i];
+  snprintf(name, len, "%s", n.c_str());
+  const ParamSpec& s = h->params.at(n);
+  *dtype = s.dtype;
+  *numel = s.numel;
+  return PDM_OK;
+}
+
+int pdm_uvit_set_param(pdm_uvit* h, const char* name, const void* dev_ptr, int dtype, long long numel) {
+  if (!h || !name) return fail(PDM_ERR_ARG, "pdm_uvit_set_param: null argument");
+  auto it = h->params.find(name);
+  if (it == h->params.end()) return fail(PDM_ERR_ARG, std::string("pdm_uvit_set_param: unexpected key ") + name);
+  if (it->second.dtype != dtype || it->second.numel != numel)
+    return fail(PDM_ERR_ARG, std::string("pdm_uvit_set_param: dtype/size mismatch for ") + name);
+  if (((uintptr_t)dev_ptr) & 15) return fail(PDM_ERR_ARG, std::string("pdm_uvit_set_param: 16-byte alignment required for ") + name);
+  it->second.ptr = dev_ptr;
+  return PDM_OK;
+}
+
+int pdm_uvit_validate(pdm_uvit* h) {
+  if (!h) return fail(PDM_ERR_ARG, "null handle");
+  return check_ready(h);
+}
+
+int pdm_uvit_workspace_size(const pdm_uvit* h, int rows, size_t* bytes) {
+  if (!h || rows <= 0 || !bytes) return fail(PDM_ERR_ARG, "pdm_uvit_workspace_size: bad argument");
+  *bytes = layout(h, rows, nullptr).bytes;
+  return PDM_OK;
+}
+
+int pdm_uvit_forward(pdm_uvit* h, const float* x, const float* t, const int64_t* y, float* eps_pre, int rows,
+                     void* workspace, size_t workspace_bytes, void* stream) {
+  if (!h || !x || !t || !eps_pre || rows <= 0) return fail(PDM_ERR_ARG, "pdm_uvit_forward: bad argument");
+  if (h->cfg.t2i) return fail(PDM_ERR_ARG, "pdm_uvit_forward: t2i network, use pdm_uvit_t2i_forward");
+  if (h->cfg.num_classes > 0 && !y) return fail(PDM_ERR_ARG, "pdm_uvit_forward: labels required (num_classes > 0)");
+  if (h->cfg.num_classes <= 0 && y) return fail(PDM_ERR_ARG, "pdm_uvit_forward: labels given to an unconditional net");
+  PDM_TRY(check_ready(h));
+  Workspace w = layout(h, rows, (char*)workspace);
+  if (w.bytes > workspace_bytes) return fail(PDM_ERR_ARG, "pdm_uvit_forward: workspace too small");
+  Ctx c{h, (hipStream_t)stream};
+  const int D = h->D, L = h->Lx;
+  {
+    pdm::AssembleArgs a{};
+    a.img = x; a.C = h->C; a.Himg = h->cfg.img_size; a.Wimg = h->cfg.img_size; a.p = h->p;
+    a.patch_w = h->f("patch_embed.proj.weight"); a.patch_b = h->f("patch_embed.proj.bias");
+    a.t = t; a.y = y;
+    a.label_emb = h->cfg.num_classes > 0 ? h->f("label_emb.weight") : nullptr;
+    a.pos = h->f("pos_embed");
+    a.out = w.X; a.ld_out = D;
+    a.B = rows; a.D = D; a.L_total = L;
+    a.row0_patch = h->extras;
+    a.time_row = h->extras - 1;
+    a.label_row = h->cfg.num_classes > 0 ? 0 : -1;   // token order [label, time, patches] (libs/uvit.py:205-211)
+    a.ctx_row = -1;
+    PDM_CHECK(pdm::assemble_check(a));
+    PDM_HIP(pdm::assemble_launch(a, c.s));
+  }
+  const size_t MD = (size_t)rows * L * D;
+  for (int i = 0; i < h->nhalf; ++i)
+    PDM_TRY(run_block(c, "in_blocks." + std::to_string(i), w.X, rows, L, nullptr, nullptr, w.SK + i * MD, w));
+  PDM_TRY(run_block(c, "mid_block", w.X, rows, L, nullptr, nullptr, w.XB, w));
+  for (int i = 0; i < h->nhalf; ++i) {
+    const bf16* sk = h->cfg.skip ? w.SK + (h->nhalf - 1 - i) * MD : nullptr;
+    PDM_TRY(run_block(c, "out_blocks." + std::to_string(i), w.X, rows, L, w.XB, sk, w.XB, w));
+  }
+  PDM_TRY(run_head(c, w, rows, w.X, L, h->extras, "norm", "decoder_pred", h->C, h->P, h->P_pad, eps_pre, true));
+  return PDM_OK;
+}
+
+int pdm_uvit_t2i_forward(pdm_uvit* h, const float* x, const float* t, const float* context, const float* mask_token,
+                         int use_ground_truth, float* eps_pre, float* mask_pre, int rows, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  (void)h; (void)x; (void)t; (void)context; (void)mask_token; (void)use_ground_truth; (void)eps_pre;
+  (void)mask_pre; (void)rows; (void)workspace; (void)workspace_bytes; (void)stream;
+  return fail(PDM_ERR_STATE, "pdm_uvit_t2i_forward: not built yet");
+}
+
+int pdm_stage_epilogue(const pdm_stage_epilogue_args* a, void* stream) {
+  if (!a) return fail(PDM_ERR_ARG, "pdm_stage_epilogue: null args");
+  pdm::EpilogueArgs e{};
+  e.pre = a->pre; e.w = a->conv_w; e.bias = a->conv_b;
+  e.B = a->B; e.C = a->C; e.Himg = a->H; e.Wimg = a->W;
+  e.has_uncond = a->has_uncond; e.cfg_scale = a->cfg_scale;
+  e.act_tanh = a->act_tanh;
+  e.xin = a->xin; e.ax = a->ax; e.ae = a->ae;
+  e.m_out = a->m_out;
+  e.n_terms = a->n_terms;
+  for (int i = 0; i < 6; ++i) { e.T[i] = a->T[i]; e.c[i] = a->c[i]; }
+  e.cm = a->cm;
+  e.x_out = a->x_out;
+  PDM_CHECK(pdm::epilogue_check(e));
+  PDM_HIP(pdm::epilogue_launch(e, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_lincomb(float* out, int n_terms, const float* const* T, const float* c, long long n, void* stream) {
+  if (!out || n_terms < 0 || n_terms > 8 || (n_terms && (!T || !c))) return fail(PDM_ERR_ARG, "pdm_lincomb: bad argument");
+  PDM_HIP(pdm::lincomb_launch(out, n_terms, T, c, n, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_gemm_bf16(const void* A1, int lda1, const void* A2, int lda2, int K1, const void* W, const float* bias, int M,
+                  int N, int K, int epi, void* out_bf16, int ldo, float* out_f32, int ldr, int accumulate,
+                  void* stream) {
+  pdm::GemmArgs a{};
+  a.A1 = (const bf16*)A1; a.lda1 = lda1;
+  a.A2 = (const bf16*)A2; a.lda2 = lda2;
+  a.K1 = A2 ? K1 : K;
+  a.W = (const bf16*)W; a.bias = bias;
+  a.M = M; a.N = N; a.K = K;
+  a.out_bf16 = (bf16*)out_bf16; a.ldo = ldo;
+  a.out_f32 = out_f32; a.ldr = ldr;
+  a.accumulate = accumulate;
+  PDM_CHECK(pdm::gemm_check(a, epi));
+  PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_layernorm(const float* x, int ldx, const float* gamma, const float* beta, void* y, int ldy, int rows, int D,
+                  float eps, void* stream) {
+  pdm::LayerNormArgs a{};
+  a.x = x; a.ldx = ldx; a.gamma = gamma; a.beta = beta; a.y = (bf16*)y; a.ldy = ldy;
+  a.rows = rows; a.D = D; a.rows_per_group = 1; a.group_stride = 1; a.row_offset = 0; a.eps = eps;
+  PDM_CHECK(pdm::layernorm_check(a));
+  PDM_HIP(pdm::layernorm_launch(a, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_attention(const void* qkv, int ldq, void* out, int ldo, int B, int L, int H, int Dh, float scale,
+                  void* stream) {
+  pdm::AttentionArgs a{};
+  a.qkv = (const bf16*)qkv; a.ldq = ldq; a.out = (bf16*)out; a.ldo = ldo;
+  a.B = B; a.L = L; a.H = H; a.Dh = Dh; a.scale = scale;
+  PDM_CHECK(pdm::attention_check(a));
+  PDM_HIP(pdm::attention_launch(a, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_f32_to_bf16(const float* x, void* y, long long n, void* stream) {
+  if (!x || !y || n < 0) return fail(PDM_ERR_ARG, "pdm_f32_to_bf16: bad argument");
+  PDM_HIP(pdm::cast_bf16_launch(x, (bf16*)y, n, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+}  // extern "C"

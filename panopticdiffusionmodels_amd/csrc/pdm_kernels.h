@@ -1,0 +1,120 @@
+// Internal launcher declarations shared by the kernels and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace pdm {
+
+typedef __bf16 bf16;
+
+enum { EPI_BF16 = 0, EPI_GELU = 1, EPI_F32 = 2 };
+
+struct GemmArgs {
+  const bf16* A1; int lda1;   // A[:, 0:K1]
+  const bf16* A2; int lda2;   // A[:, K1:K] (may be null when K1 == K)
+  int K1;
+  const bf16* W;              // [N][K] row-major (nn.Linear weight)
+  const float* bias;          // [N] or null
+  int M, N, K;
+  bf16* out_bf16; int ldo;    // EPI_BF16 / EPI_GELU output, or optional bf16 copy for EPI_F32
+  float* out_f32; int ldr;    // EPI_F32 output (residual stream)
+  int accumulate;             // EPI_F32: out_f32 += result (residual add) instead of =
+  int a_rows_per_group;       // >0: A1 row m is read from (m / rpg) * a_group_stride + m % rpg
+  int a_group_stride;
+};
+
+const char* gemm_check(const GemmArgs& p, int epi);
+hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream);
+
+// LayerNorm over the last dim of fp32 rows -> bf16.  Row r of the output is row
+// (r / rows_per_group) * group_stride + row_offset + (r % rows_per_group) of the input.
+struct LayerNormArgs {
+  const float* x; int ldx;
+  const float* gamma; const float* beta;
+  bf16* y; int ldy;
+  int rows, D;
+  int rows_per_group, group_stride, row_offset;   // row gather (final norm over patch tokens only)
+  float eps;
+};
+const char* layernorm_check(const LayerNormArgs& p);
+hipError_t layernorm_launch(const LayerNormArgs& p, hipStream_t stream);
+
+// Fused multi-head attention over a packed qkv buffer [B*L, 3*D] (layout (3, H, Dh) per token, as
+// libs/uvit.py:71 rearranges it) -> out [B*L, D] (layout (H, Dh)).  No mask; softmax scale Dh^-1/2.
+struct AttentionArgs {
+  const bf16* qkv; int ldq;   // row stride of qkv (elements)
+  bf16* out; int ldo;
+  int B, L, H, Dh;
+  float scale;
+};
+const char* attention_check(const AttentionArgs& p);
+hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream);
+
+// Token assembly (libs/uvit.py:201-212, libs/uvit_t2i.py:382-409):
+// out[b, row] for the sequence [label?][time][context x n_ctx?][patches] + pos_embed, fp32.
+struct AssembleArgs {
+  const float* img;           // [B, C, Himg, Wimg]
+  int C, Himg, Wimg, p;
+  const float* patch_w;       // [D, C*p*p] fp32
+  const float* patch_b;       // [D]
+  const float* t;             // [B] timesteps (already scaled as the net receives them)
+  const float* time_emb;      // optional precomputed time tokens [B, D] (mlp_time_embed); null -> sinusoid
+  const int64_t* y;           // [B] labels or null
+  const float* label_emb;     // [num_classes, D]
+  const float* ctx_tokens;    // [B, n_ctx, D] already embedded context tokens, or null
+  int n_ctx;
+  const float* pos;           // [L_pos, D]; rows used = tokens of this sequence
+  float* out; int ld_out;     // [B, L_total, D] with row stride ld_out (elements)
+  int B, D, L_total;          // tokens per sample written
+  int row0_patch;             // index of the first patch token
+  int time_row;               // index of the time token (-1: none)
+  int label_row;              // index of the label token (-1: none)
+  int ctx_row;                // index of the first context token (-1: none)
+};
+const char* assemble_check(const AssembleArgs& p);
+hipError_t assemble_launch(const AssembleArgs& p, hipStream_t stream);
+
+// decoder_pred (D -> P = p*p*C, bias) on bf16 patch rows + unpatchify scatter to NCHW fp32
+// (libs/uvit.py:182,225-228 and unpatchify 46-51; column order (p1, p2, C)).
+struct HeadArgs {
+  const bf16* x; int ldx;     // [B*N, D] rows (already LayerNorm-ed), N = (H/p)*(W/p)
+  const bf16* W;              // [P_pad][D] (rows >= P are zero)
+  const float* bias;          // [P]
+  float* out;                 // [B, C, H, W]
+  int B, D, C, p, Himg, Wimg, P, P_pad;
+  int act_tanh;               // apply tanh after (used for no-conv mask heads only)
+};
+const char* head_check(const HeadArgs& p);
+hipError_t head_launch(const HeadArgs& p, hipStream_t stream);
+
+// Final 3x3 conv (optional) + classifier-free guidance + solver stage epilogue, fp32, [B, C, H, W].
+//   e   = conv(pre[b])            (identity if w == null)
+//   if act_tanh: e = tanh(e)              (per call, before the CFG combine)
+//   if uncond: e = e + s * (e - act(conv(pre[b + B])))
+//   m   = ax * xin + ae * e        (x0 conversion for data prediction; ax = 0, ae = 1 for noise)
+//   m_out = m (if non-null);  x_out = sum_i c_i * T_i + cm * m  (if non-null)
+struct EpilogueArgs {
+  const float* pre;           // [B or 2B, C, H, W]
+  const float* w; const float* bias;   // conv [C, C, 3, 3], [C]
+  int B, C, Himg, Wimg;
+  int has_uncond; float cfg_scale;
+  int act_tanh;
+  const float* xin; float ax, ae;
+  float* m_out;
+  int n_terms; const float* T[6]; float c[6]; float cm;
+  float* x_out;
+};
+const char* epilogue_check(const EpilogueArgs& p);
+hipError_t epilogue_launch(const EpilogueArgs& p, hipStream_t stream);
+
+hipError_t cast_bf16_launch(const float* x, bf16* y, long long n, hipStream_t stream);
+
+// out = sum_i c_i * T_i over n elements (fp32); used by the generic solver path.
+hipError_t lincomb_launch(float* out, int n_terms, const float* const* T, const float* c, long long n, hipStream_t stream);
+
+// Strided row copy fp32: dst[r*ldd + j] = src[r*lds + j], j < D, r < rows (t2i mask stream concat).
+hipError_t rowcopy_launch(float* dst, int ldd, const float* src, int lds, int rows, int D, int rows_per_group,
+                          int dst_group_stride, int src_group_stride, hipStream_t stream);
+
+}  // namespace pdm

@@ -1,0 +1,129 @@
+"""Binding between an nn.Module holding the reference-named parameters and a pdm_uvit handle.
+
+The module keeps fp32 parameters under the reference's state_dict keys (so `load_state_dict` of a
+reference checkpoint works unchanged, eval_ldm_discrete.py:46).  On first GPU use the parameters are
+packed once into the layouts libpdm expects (Linear weights -> bf16 [out, in]; decoder heads padded to a
+multiple of 16 rows; conv / embedding tables fp32) and their device addresses are registered with the
+handle.  Any load_state_dict / .to() invalidates the packed copy.
+"""
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+
+def cfg_struct(kw, t2i):
+    c = _lib.PdmUvitCfg()
+    D = int(kw["embed_dim"])
+    c.img_size = int(kw["img_size"])
+    c.patch_size = int(kw["patch_size"])
+    c.in_chans = int(kw.get("in_chans", 3))
+    c.embed_dim = D
+    c.depth = int(kw["depth"])
+    c.num_heads = int(kw["num_heads"])
+    c.mlp_hidden = int(D * kw.get("mlp_ratio", 4.0))
+    c.num_classes = int(kw.get("num_classes", -1)) if not t2i else -1
+    c.conv = int(bool(kw.get("conv", True)))
+    c.skip = int(bool(kw.get("skip", True)))
+    c.qkv_bias = int(bool(kw.get("qkv_bias", False)))
+    c.mlp_time_embed = int(bool(kw.get("mlp_time_embed", False)))
+    c.t2i = int(t2i)
+    c.clip_dim = int(kw.get("clip_dim", 768)) if t2i else 0
+    c.num_clip_token = int(kw.get("num_clip_token", 77)) if t2i else 0
+    c.separate = int(bool(kw.get("separate", False))) if t2i else 0
+    c.enable_panoptic = int(bool(kw.get("enable_panoptic", True))) if t2i else 0
+    c.num_panoptic_class = int(kw.get("num_panoptic_class", 8)) if t2i else 0
+    return c
+
+
+class NativeHandle:
+    """Owns a pdm_uvit handle plus the packed device copies of the weights it points at."""
+
+    def __init__(self, module, cfg):
+        lib = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(lib.pdm_uvit_create(ctypes.byref(cfg), ctypes.byref(h)), "pdm_uvit_create")
+        self.h = h
+        self.lib = lib
+        self.cfg = cfg
+        self.packed = {}
+        self.ws = None
+        sd = module.state_dict()
+        dev = next(iter(sd.values())).device
+        n = lib.pdm_uvit_param_count(h)
+        buf = ctypes.create_string_buffer(256)
+        for i in range(n):
+            dt = ctypes.c_int()
+            numel = ctypes.c_longlong()
+            _lib.check(lib.pdm_uvit_param_info(h, i, buf, 256, ctypes.byref(dt), ctypes.byref(numel)))
+            name = buf.value.decode()
+            t = self._pack(sd, name, dt.value, numel.value, dev)
+            self.packed[name] = t
+            _lib.check(lib.pdm_uvit_set_param(h, name.encode(), ctypes.c_void_p(t.data_ptr()), dt.value, t.numel()),
+                       "pdm_uvit_set_param")
+        _lib.check(lib.pdm_uvit_validate(h), "pdm_uvit_validate")
+
+    @staticmethod
+    def _pack(sd, name, dtype, numel, dev):
+        if name not in sd:
+            raise RuntimeError(f"parameter {name!r} missing from the module state_dict")
+        src = sd[name].detach()
+        if name.startswith("zero_convs."):
+            src = src.reshape(src.shape[0], -1)
+        if name in ("decoder_pred.weight", "decoder_pred_mask.weight"):
+            P, D = src.shape
+            Ppad = (P + 15) // 16 * 16
+            pad = torch.zeros(Ppad, D, dtype=src.dtype, device=src.device)
+            pad[:P] = src
+            src = pad
+        t = src.to(device=dev, dtype=torch.bfloat16 if dtype == _lib.PDM_BF16 else torch.float32).contiguous()
+        t = t.reshape(-1)
+        if t.numel() != numel:
+            raise RuntimeError(f"parameter {name!r}: {t.numel()} elements, the HIP layout expects {numel}")
+        return t
+
+    def workspace(self, rows, device):
+        need = ctypes.c_size_t()
+        _lib.check(self.lib.pdm_uvit_workspace_size(self.h, rows, ctypes.byref(need)), "pdm_uvit_workspace_size")
+        if self.ws is None or self.ws.numel() < need.value or self.ws.device != device:
+            self.ws = torch.empty(need.value, dtype=torch.uint8, device=device)
+        return self.ws
+
+    def __del__(self):
+        try:
+            self.lib.pdm_uvit_destroy(self.h)
+        except Exception:
+            pass
+
+
+class HipNet(nn.Module):
+    """Base class: lazily (re)builds the native handle for the module's current parameters."""
+
+    _t2i = False
+
+    def __init__(self):
+        super().__init__()
+        self._native = None
+
+    def _native_cfg_kwargs(self):
+        raise NotImplementedError
+
+    def invalidate(self):
+        self._native = None
+
+    def _apply(self, fn, *args, **kwargs):
+        self._native = None
+        return super()._apply(fn, *args, **kwargs)
+
+    def load_state_dict(self, state_dict, strict=True, *args, **kwargs):
+        self._native = None
+        return super().load_state_dict(state_dict, strict, *args, **kwargs)
+
+    def native(self):
+        if self._native is None:
+            p = next(self.parameters())
+            _lib.require_gpu(p)
+            self._native = NativeHandle(self, cfg_struct(self._native_cfg_kwargs(), self._t2i))
+        return self._native

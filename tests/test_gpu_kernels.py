@@ -1,0 +1,137 @@
+"""Per-kernel parity on the GPU: every libpdm kernel vs a plain fp32 PyTorch reference of the same op on
+the same (bf16-rounded) inputs.  Tolerances: bf16 outputs rel-L2 <= 1e-2 (one rounding of O(1) data),
+fp32 outputs from bf16 operands rel-L2 <= 2e-3."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.double()
+    b = b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from panopticdiffusionmodels_amd import _lib
+    _lib.load()
+    return _lib
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 256, 512), (25800 // 8, 1024, 1024), (77, 64, 64),
+                                   (1000, 192, 256), (4096, 3456, 1152), (129, 4608, 1152)])
+@pytest.mark.parametrize("epi", ["bf16", "gelu", "f32", "f32acc"])
+def test_gemm(lib, M, N, K, epi):
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    ref = a.float() @ w.float().t() + bias
+    if epi == "bf16":
+        out = lib.gemm(a, w, bias, lib.EPI_BF16)
+        assert rel(out.float(), ref) < 1e-2
+    elif epi == "gelu":
+        out = lib.gemm(a, w, bias, lib.EPI_GELU)
+        assert rel(out.float(), F.gelu(ref)) < 1e-2
+    elif epi == "f32":
+        out = lib.gemm(a, w, bias, lib.EPI_F32)
+        assert rel(out, ref) < 2e-3
+    else:
+        r0 = torch.randn(M, N, device="cuda", generator=g)
+        out = lib.gemm(a, w, bias, lib.EPI_F32, out_f32=r0.clone(), accumulate=True)
+        assert rel(out, ref + r0) < 2e-3
+
+
+def test_gemm_split_k(lib):
+    g = torch.Generator(device="cuda").manual_seed(1)
+    M, D = 517, 256
+    x = torch.randn(M, D, device="cuda", generator=g).bfloat16()
+    s = torch.randn(M, D, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(D, 2 * D, device="cuda", generator=g) * (2 * D) ** -0.5).bfloat16()
+    b = torch.randn(D, device="cuda", generator=g)
+    out = lib.gemm(x, w, b, lib.EPI_F32, a2=s)
+    ref = torch.cat([x, s], dim=1).float() @ w.float().t() + b
+    assert rel(out, ref) < 2e-3
+
+
+def test_gemm_bad_shape(lib):
+    a = torch.zeros(16, 100, device="cuda", dtype=torch.bfloat16)
+    w = torch.zeros(128, 100, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        lib.gemm(a, w)
+
+
+@pytest.mark.parametrize("rows,D", [(1, 64), (258, 1024), (1000, 1152), (33, 512), (7, 576)])
+def test_layernorm(lib, rows, D):
+    g = torch.Generator(device="cuda").manual_seed(rows + D)
+    x = torch.randn(rows, D, device="cuda", generator=g) * 3 + 1
+    gm = torch.randn(D, device="cuda", generator=g)
+    bt = torch.randn(D, device="cuda", generator=g)
+    y = lib.layernorm(x, gm, bt)
+    ref = F.layer_norm(x, (D,), gm, bt, eps=1e-5)
+    assert rel(y.float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("L", [66, 257, 258, 334, 590])
+@pytest.mark.parametrize("Dh", [32, 64, 72])
+def test_attention(lib, L, Dh):
+    H, B = 3, 2
+    D = H * Dh
+    g = torch.Generator(device="cuda").manual_seed(L * 10 + Dh)
+    qkv = (torch.randn(B * L, 3 * D, device="cuda", generator=g) * 1.5).bfloat16()
+    out = lib.attention(qkv, B, L, H, Dh)
+    q, k, v = qkv.float().reshape(B, L, 3, H, Dh).permute(2, 0, 3, 1, 4)
+    ref = torch.softmax(q @ k.transpose(-1, -2) * Dh ** -0.5, dim=-1) @ v
+    ref = ref.permute(0, 2, 1, 3).reshape(B * L, D)
+    assert rel(out.float(), ref) < 1e-2
+
+
+def test_attention_spiky(lib):
+    """A key row far above the rest forces a late running-max jump (online-softmax rescale branch)."""
+    B, L, H, Dh = 1, 258, 2, 64
+    D = H * Dh
+    g = torch.Generator(device="cuda").manual_seed(0)
+    qkv = torch.randn(B * L, 3 * D, device="cuda", generator=g)
+    qkv[200, D:2 * D] *= 8.0   # key 200 (third chunk) dominates
+    qkv = qkv.bfloat16()
+    out = lib.attention(qkv, B, L, H, Dh)
+    q, k, v = qkv.float().reshape(B, L, 3, H, Dh).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(q @ k.transpose(-1, -2) * Dh ** -0.5, dim=-1) @ v).permute(0, 2, 1, 3).reshape(B * L, D)
+    assert rel(out.float(), ref) < 1e-2
+
+
+def test_stage_epilogue(lib):
+    g = torch.Generator(device="cuda").manual_seed(3)
+    B, C, H, W = 3, 4, 8, 8
+    pre = torch.randn(2 * B, C, H, W, device="cuda", generator=g)
+    w = torch.randn(C, C, 3, 3, device="cuda", generator=g) * 0.2
+    b = torch.randn(C, device="cuda", generator=g)
+    xin = torch.randn(B, C, H, W, device="cuda", generator=g)
+    T0 = torch.randn(B, C, H, W, device="cuda", generator=g)
+    T1 = torch.randn(B, C, H, W, device="cuda", generator=g)
+    m = torch.empty_like(xin)
+    xo = torch.empty_like(xin)
+    lib.stage_epilogue(pre, B, conv_w=w, conv_b=b, cfg_scale=0.4, xin=xin, ax=1.7, ae=-0.3, m_out=m,
+                       terms=[T0, T1], coeffs=[0.5, -2.0], cm=0.25, x_out=xo)
+    c = F.conv2d(pre[:B], w, b, padding=1)
+    u = F.conv2d(pre[B:], w, b, padding=1)
+    e = c + 0.4 * (c - u)
+    mr = 1.7 * xin - 0.3 * e
+    assert rel(m, mr) < 1e-5
+    assert rel(xo, 0.5 * T0 - 2.0 * T1 + 0.25 * mr) < 1e-5
+    # tanh per call before the combine (mask head)
+    lib.stage_epilogue(pre, B, conv_w=w, conv_b=b, cfg_scale=1.0, act_tanh=True, m_out=m)
+    mt = torch.tanh(c) + 1.0 * (torch.tanh(c) - torch.tanh(u))
+    assert rel(m, mt) < 1e-5
+
+
+def test_lincomb(lib):
+    g = torch.Generator(device="cuda").manual_seed(4)
+    ts = [torch.randn(5, 4, 7, 9, device="cuda", generator=g) for _ in range(4)]
+    out = lib.lincomb(ts, [1.0, -0.5, 0.25, 3.0])
+    assert rel(out, ts[0] - 0.5 * ts[1] + 0.25 * ts[2] + 3 * ts[3]) < 1e-6

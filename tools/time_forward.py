@@ -1,0 +1,36 @@
+"""Quick timing of one U-ViT forward at a given batch (dev tool)."""
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from panopticdiffusionmodels_amd import configs, weights  # noqa: E402
+from panopticdiffusionmodels_amd.utils import get_nnet  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else "imagenet256_uvit_large"
+rows = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+dev = torch.device("cuda")
+cfg = configs.nnet_kwargs(name)
+sd = weights.nnet_state_dict(cfg, seed=0, device=dev)
+net = get_nnet(**cfg).to(dev)
+net.load_state_dict(sd)
+zs = configs.get_config(name)["z_shape"]
+x = torch.randn(rows, *zs, device=dev)
+t = torch.rand(rows, device=dev) * 999
+y = torch.randint(0, 1000, (rows,), device=dev) if cfg.get("num_classes", -1) > 0 else None
+with torch.no_grad():
+    for _ in range(3):
+        net.forward_pre(x, t, y)
+    torch.cuda.synchronize()
+    n = 10
+    t0 = time.perf_counter()
+    for _ in range(n):
+        net.forward_pre(x, t, y)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / n
+D, depth = cfg["embed_dim"], cfg["depth"]
+L = (cfg["img_size"] // cfg["patch_size"]) ** 2 + (2 if cfg.get("num_classes", -1) > 0 else 1)
+gemm_flops = rows * L * (depth + 1) * 2 * (3 * D * D + D * D + 8 * D * D) + rows * L * (depth // 2) * 2 * 2 * D * D
+attn_flops = rows * (depth + 1) * 4 * L * L * D
+print(f"{name} rows={rows}: {dt*1e3:.2f} ms/forward, {(gemm_flops+attn_flops)/dt/1e12:.1f} TFLOP/s")
