@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the sampling hot path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): configs/imagenet256_uvit_large.py — U-ViT-L/2, 50-step DPM-Solver
+(dpm_solver_pytorch fast, eval_ldm.py:93-108), classifier-free guidance 0.4, KL-f8 decode to 256x256,
+bf16 compute, synthetic seeded weights and inputs.  One "step" = one batch of B images per GPU:
+z_T -> 50 NFE (each = one 2B-row U-ViT forward + fused CFG/solver epilogue) -> all-gather of the final
+latents over RCCL (N > 1) -> decode of the rank's own B latents.
+
+  python bench.py [--gpus N --steps K --warmup W --batch B]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL over xGMI)
+
+Rank 0 prints one JSON line.  `value` = images/sec of the whole job = N*B*K / max-over-ranks wall time.
+The CPU baseline (rank 0, N = 1 only, after the GPU timing) times the fp32 CPU oracle on a bounded sample
+of the same workload (a few CFG forwards + one decode) and extrapolates to images/sec.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from panopticdiffusionmodels_amd import configs, weights  # noqa: E402
+from panopticdiffusionmodels_amd.libs.autoencoder import get_model  # noqa: E402
+from panopticdiffusionmodels_amd.sampler import ClassCondSampler  # noqa: E402
+from panopticdiffusionmodels_amd.utils import get_nnet  # noqa: E402
+
+PEAK_BF16 = 2.5e15   # dense bf16 MFMA, MI355X_MICROARCH.md chip table
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64, help="images per GPU per step")
+    ap.add_argument("--config", default="imagenet256_uvit_large")
+    ap.add_argument("--no-decode", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-nfe", type=int, default=4, help="CFG forwards timed for the CPU baseline")
+    return ap.parse_args()
+
+
+def gemm_flops_per_forward(cfg, rows):
+    D, depth = cfg["embed_dim"], cfg["depth"]
+    Hd = int(D * cfg.get("mlp_ratio", 4))
+    L = (cfg["img_size"] // cfg["patch_size"]) ** 2 + (2 if cfg.get("num_classes", -1) > 0 else 1)
+    M = rows * L
+    per_block = 2 * M * (3 * D * D + D * D + 2 * D * Hd)
+    return (depth + 1) * per_block + (depth // 2) * 2 * M * 2 * D * D
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    full = configs.get_config(args.config)
+    ncfg = dict(full["nnet"])
+    B = args.batch
+    # weights: seeded synthetic (no checkpoints offline); identical on every rank
+    sd = weights.nnet_state_dict(ncfg, seed=0, init="reference", device=dev)
+    net = get_nnet(**ncfg).to(dev).eval()
+    net.load_state_dict(sd)
+    del sd
+    null_label = ncfg["num_classes"] - 1 if ncfg.get("num_classes", -1) > 0 else None
+    sampler = ClassCondSampler(net, front_end=full["front_end"], cfg_scale=full["cfg_scale"], null_label=null_label,
+                               steps=full["sample_steps"], eps=full.get("eps"), use_graph=not args.no_graph)
+    ae = get_model(None, scale_factor=full.get("scale_factor", 0.18215), seed=1).to(dev) if not args.no_decode else None
+
+    # inputs for every (warmup + timed) step, generated per GLOBAL sample index and resident in HBM
+    nsteps = args.warmup + args.steps
+    zs, ys = [], []
+    zshape = full["z_shape"]
+    for s in range(nsteps):
+        g = torch.Generator().manual_seed(1234 + (s * world + rank))
+        zs.append(torch.randn(B, *zshape, generator=g).to(dev))
+        ys.append(torch.randint(0, 1000, (B,), generator=g).to(dev) if null_label is not None else None)
+    gathered = torch.empty(world * B, *zshape, device=dev) if world > 1 else None
+
+    def one_step(s):
+        z = sampler.sample(zs[s], ys[s])
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, z)
+        if ae is not None:
+            img = ae.decode(z)
+            return img
+        return z
+
+    for s in range(args.warmup):
+        one_step(s)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.warmup, nsteps):
+        out = one_step(s)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out).all()
+
+    # ---- roofline of the dominant kernel (the bf16 GEMM family): HIP events around every GEMM launch of one
+    # CFG forward, recorded on the stream the kernels run on (the native driver's profiling hook)
+    roof = net_gemm_roofline(net, sampler, zs[0], ys[0], ncfg, B)
+
+    images = world * B * args.steps
+    value = images / elapsed
+    res = {
+        "metric": "images/sec (whole node), ImageNet256 U-ViT-L 50-step DPM-Solver, 1/2/4/8 GPU",
+        "value": round(value, 3),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (seeded random-init U-ViT-L/2 + KL-f8 weights, z_T ~ N(0,1), labels U{0..999})",
+        "config": {"workload": f"{args.config}: 50-step DPM-Solver (fast, order 3), CFG {full['cfg_scale']}, "
+                               f"{'+ KL-f8 decode 256x256' if ae is not None else 'no decode'}",
+                   "model": "U-ViT-L/2", "per_gpu_batch": B, "global_batch": world * B,
+                   "nfe": sampler.nfe, "hip_graph": not args.no_graph, "parallelism": f"dp{world} (batch-sharded)"},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        res["cpu_baseline"] = cpu_baseline(full, ncfg, args.cpu_nfe, ae is not None)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def net_gemm_roofline(net, sampler, z, y, ncfg, B):
+    """Average duration of the GEMM kernel over one CFG forward of the benchmark batch (2B rows), from HIP
+    events recorded by libpdm around each GEMM launch on the launch stream."""
+    from panopticdiffusionmodels_amd import _lib
+    nat = net.native()
+    rows = 2 * B if sampler.cfg else B
+    x = torch.cat([z, z]) if sampler.cfg else z
+    t = torch.full((rows,), 500.0, device=z.device)
+    yy = torch.cat([y, torch.full_like(y, sampler.null_label)]) if (sampler.cfg and y is not None) else y
+    prof = _lib.GemmProfiler(nat, max_launches=512)
+    with torch.no_grad():
+        net.forward_pre(x, t, yy)          # warm
+        prof.enable()
+        net.forward_pre(x, t, yy)
+        prof.disable()
+    torch.cuda.synchronize()
+    times_ms, flops = prof.read()
+    n = len(times_ms)
+    tot_t = sum(times_ms) / 1e3
+    tot_f = sum(flops)
+    achieved = tot_f / tot_t
+    return {"bound": "mfma", "kernel": "gemm_bf16_kernel<*> (all U-ViT linear layers)",
+            "achieved": round(achieved / 1e12, 1), "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_BF16, 4), "traffic": None,
+            "launches_per_forward": n, "avg_launch_ms": round(tot_t / n * 1e3, 4),
+            "flops_per_launch": round(tot_f / n), "flops_per_forward_check": gemm_flops_per_forward(ncfg, rows)}
+
+
+def cpu_baseline(full, ncfg, n_fwd, with_decode):
+    """fp32 CPU oracle (oracle/uvit_ref.py, oracle/autoencoder_ref.py) on the host cores, bounded sample:
+    `n_fwd` CFG forwards at 2 rows (1 image) + one 256x256 decode, extrapolated to 50 NFE per image."""
+    from oracle import autoencoder_ref, uvit_ref
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, 16)   # the GPU box's CPU share
+    torch.set_num_threads(cores)
+    kw = dict(ncfg)
+    kw.pop("name")
+    sd = weights.nnet_state_dict(ncfg, seed=0, init="reference")
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, *full["z_shape"], generator=g)
+    y = torch.tensor([1, 1000])
+    t = torch.full((2,), 500.0)
+    with torch.no_grad():
+        uvit_ref.uvit_forward(sd, kw, x, t, y)  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(n_fwd):
+            uvit_ref.uvit_forward(sd, kw, x, t, y)
+        t_fwd = (time.perf_counter() - t0) / n_fwd
+        t_dec = 0.0
+        if with_decode:
+            dsd = weights.decoder_state_dict(seed=1)
+            z = torch.randn(1, 4, 32, 32, generator=g)
+            t0 = time.perf_counter()
+            autoencoder_ref.decode(dsd, z)
+            t_dec = time.perf_counter() - t0
+    per_img = full["sample_steps"] * t_fwd + t_dec
+    try:
+        model = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":", 1)[1].strip()
+    except Exception:
+        model = "unknown"
+    return {"value": round(1.0 / per_img, 5), "unit": "images/sec", "cores": cores, "kind": "port",
+            "cpu": model,
+            "sample": f"{n_fwd} CFG forwards of U-ViT-L/2 at 2 rows (1 image) = {t_fwd:.3f} s each, "
+                      f"+ 1 KL-f8 decode 256x256 = {t_dec:.2f} s; images/sec = 1 / (50 NFE x forward + decode)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -82,6 +82,13 @@ int pdm_uvit_t2i_forward(pdm_uvit* h, const float* x, const float* t, const floa
                          const float* mask_token, int use_ground_truth, float* eps_pre, float* mask_pre,
                          int rows, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Profiling hook (bench.py roofline): when enabled with max_launches > 0, every GEMM launch of the
+ * following forwards is bracketed by HIP events recorded on the launch stream (events are created here,
+ * the only entry points that create resources; profile_read synchronises on them).  profile_read returns,
+ * for the most recent forward, each GEMM's duration (ms) and algorithmic FLOPs (2 M N K). */
+int pdm_uvit_profile(pdm_uvit* h, int max_launches);
+int pdm_uvit_profile_read(pdm_uvit* h, float* ms, double* flops, int cap, int* n);
+
 /* ---- solver / guidance epilogue ------------------------------------------------------------------
  * final_layer conv3x3 (libs/uvit.py:183,229) + CFG combine (eval_ldm_discrete.py:77, eval_ldm.py:71,
  * train_t2i_discrete.py:429-431) + optional tanh (libs/uvit_t2i.py:513) + the DPM-Solver stage
@@ -90,7 +97,8 @@ int pdm_uvit_t2i_forward(pdm_uvit* h, const float* x, const float* t, const floa
  *   e = act(conv(pre[b])) (conv skipped if conv_w == NULL)
  *   if has_uncond: e += cfg_scale * (e - act(conv(pre[b+B])))
  *   m = ax * xin + ae * e   (xin may be NULL -> m = ae * e);   m_out = m (if not NULL)
- *   x_out = cm * m + sum_i c[i] * T[i]   (if not NULL)                                            */
+ *   x_out = cm * m + sum_i c[i] * T[i]   (if not NULL; also copied to x_out2 / x_out3 when not NULL:
+ *   the next model input is written straight into both CFG halves of the batched input)            */
 typedef struct pdm_stage_epilogue_args {
   const float* pre;
   const float* conv_w; const float* conv_b;
@@ -100,7 +108,7 @@ typedef struct pdm_stage_epilogue_args {
   const float* xin; float ax, ae;
   float* m_out;
   int n_terms; const float* T[6]; float c[6]; float cm;
-  float* x_out;
+  float* x_out; float* x_out2; float* x_out3;
 } pdm_stage_epilogue_args;
 int pdm_stage_epilogue(const pdm_stage_epilogue_args* a, void* stream);
 

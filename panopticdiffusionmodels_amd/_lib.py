@@ -31,7 +31,7 @@ class PdmStageEpilogueArgs(ctypes.Structure):
         ("xin", ctypes.c_void_p), ("ax", ctypes.c_float), ("ae", ctypes.c_float),
         ("m_out", ctypes.c_void_p),
         ("n_terms", ctypes.c_int), ("T", ctypes.c_void_p * 6), ("c", ctypes.c_float * 6), ("cm", ctypes.c_float),
-        ("x_out", ctypes.c_void_p),
+        ("x_out", ctypes.c_void_p), ("x_out2", ctypes.c_void_p), ("x_out3", ctypes.c_void_p),
     ]
 
 
@@ -54,6 +54,10 @@ _SIGS = {
     "pdm_uvit_t2i_forward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "pdm_uvit_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "pdm_uvit_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
+                                             ctypes.POINTER(ctypes.c_double), ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_int)]),
     "pdm_stage_epilogue": (ctypes.c_int, [ctypes.POINTER(PdmStageEpilogueArgs), ctypes.c_void_p]),
     "pdm_lincomb": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                    ctypes.POINTER(ctypes.c_float), ctypes.c_longlong, ctypes.c_void_p]),
@@ -173,7 +177,7 @@ def lincomb(terms, coeffs, out=None):
 
 
 def stage_epilogue(pre, B, conv_w=None, conv_b=None, cfg_scale=None, act_tanh=False, xin=None, ax=0.0, ae=1.0,
-                   m_out=None, terms=(), coeffs=(), cm=0.0, x_out=None):
+                   m_out=None, terms=(), coeffs=(), cm=0.0, x_out=None, x_out2=None, x_out3=None):
     """See pdm_stage_epilogue in include/pdm.h.  pre [B or 2B, C, H, W] fp32 contiguous."""
     lib = load()
     require_gpu(pre)
@@ -197,4 +201,28 @@ def stage_epilogue(pre, B, conv_w=None, conv_b=None, cfg_scale=None, act_tanh=Fa
         a.c[i] = float(c)
     a.cm = float(cm)
     a.x_out = x_out.data_ptr() if x_out is not None else None
+    a.x_out2 = x_out2.data_ptr() if x_out2 is not None else None
+    a.x_out3 = x_out3.data_ptr() if x_out3 is not None else None
     check(lib.pdm_stage_epilogue(ctypes.byref(a), stream_ptr(pre.device)), "pdm_stage_epilogue")
+
+
+class GemmProfiler:
+    """HIP-event timing of every GEMM launch of a forward (pdm_uvit_profile)."""
+
+    def __init__(self, native, max_launches=512):
+        self.nat = native
+        self.cap = max_launches
+
+    def enable(self):
+        check(self.nat.lib.pdm_uvit_profile(self.nat.h, self.cap), "pdm_uvit_profile")
+
+    def disable(self):
+        check(self.nat.lib.pdm_uvit_profile(self.nat.h, 0), "pdm_uvit_profile")
+
+    def read(self):
+        ms = (ctypes.c_float * self.cap)()
+        fl = (ctypes.c_double * self.cap)()
+        n = ctypes.c_int()
+        check(self.nat.lib.pdm_uvit_profile_read(self.nat.h, ms, fl, self.cap, ctypes.byref(n)), "pdm_uvit_profile_read")
+        k = min(n.value, self.cap)
+        return [ms[i] for i in range(k)], [fl[i] for i in range(k)]

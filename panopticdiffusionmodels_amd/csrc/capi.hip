@@ -52,6 +52,11 @@ struct pdm_uvit {
   int D, H, Dh, Hid, C, p, n_patch, extras, Lx, Lm, P, P_pad, K, PK, PK_pad, depth, nhalf;
   std::vector<std::string> order;
   std::map<std::string, ParamSpec> params;
+  // profiling hook: events around every GEMM launch of the last forward (bench roofline)
+  mutable std::vector<hipEvent_t> prof_ev;
+  mutable std::vector<double> prof_flops;
+  mutable int prof_n = 0;
+  mutable bool prof_on = false;
 
   void add(const std::string& name, int dtype, long long numel) {
     order.push_back(name);
@@ -162,7 +167,15 @@ int gemm(const Ctx& c, const bf16* A, int lda, const bf16* W, const float* bias,
   a.accumulate = accumulate;
   a.a_rows_per_group = a_rpg; a.a_group_stride = a_gs;
   PDM_CHECK(pdm::gemm_check(a, epi));
+  const pdm_uvit* h = c.h;
+  const bool prof = h->prof_on && 2 * (h->prof_n + 1) <= (int)h->prof_ev.size();
+  if (prof) PDM_HIP(hipEventRecord(h->prof_ev[2 * h->prof_n], c.s));
   PDM_HIP(pdm::gemm_launch(a, epi, c.s));
+  if (prof) {
+    PDM_HIP(hipEventRecord(h->prof_ev[2 * h->prof_n + 1], c.s));
+    h->prof_flops[h->prof_n] = 2.0 * M * N * K;
+    ++h->prof_n;
+  }
   return PDM_OK;
 }
 
@@ -225,22 +238,37 @@ int check_ready(pdm_uvit* h) {
   return PDM_OK;
 }
 
-int run_head(const Ctx& c, const Workspace& w, int rows, const float* Xsrc, int L_src, int row_off,
-             const std::string& norm, const std::string& head, int Cout, int P, int P_pad, float* out, bool ln) {
+// decoder_pred-style head on bf16 token rows: token (b, i) is row b * group_stride + row_offset + i of `hin`.
+int run_head(const Ctx& c, const bf16* hin, int group_stride, int row_offset, int rows, const std::string& head,
+             int Cout, int P, int P_pad, float* out) {
   const pdm_uvit* h = c.h;
-  const int D = h->D;
-  const bf16* hin = w.HEADIN;
-  if (ln) {
-    PDM_TRY(layernorm(c, Xsrc, norm, w.HEADIN, rows * h->n_patch, h->n_patch, L_src, row_off));
-  }
   pdm::HeadArgs a{};
-  a.x = hin; a.ldx = D;
+  a.x = hin; a.ldx = h->D;
+  a.in_group_stride = group_stride; a.in_row_offset = row_offset;
   a.W = h->w(head + ".weight"); a.bias = h->f(head + ".bias");
   a.out = out;
-  a.B = rows; a.D = D; a.C = Cout; a.p = h->p; a.Himg = h->cfg.img_size; a.Wimg = h->cfg.img_size;
+  a.B = rows; a.D = h->D; a.C = Cout; a.p = h->p; a.Himg = h->cfg.img_size; a.Wimg = h->cfg.img_size;
   a.P = P; a.P_pad = P_pad; a.act_tanh = 0;
   PDM_CHECK(pdm::head_check(a));
   PDM_HIP(pdm::head_launch(a, c.s));
+  return PDM_OK;
+}
+
+// final LayerNorm over the patch tokens of X (rows extras .. L-1 of each sequence) -> HEADIN, optionally
+// adding fp32 rows `add` (use_ground_truth: libs/uvit_t2i.py:486-494) after the affine
+int final_norm(const Ctx& c, const Workspace& w, int rows, const float* X, int L, const float* add = nullptr,
+               int add_gs = 0, int add_off = 0) {
+  const pdm_uvit* h = c.h;
+  pdm::LayerNormArgs a{};
+  a.x = X; a.ldx = h->D;
+  a.gamma = h->f("norm.weight"); a.beta = h->f("norm.bias");
+  a.y = w.HEADIN; a.ldy = h->D;
+  a.rows = rows * h->n_patch; a.D = h->D;
+  a.rows_per_group = h->n_patch; a.group_stride = L; a.row_offset = h->extras;
+  a.eps = 1e-5f;
+  a.add = add; a.add_ld = h->D; a.add_group_stride = add_gs; a.add_row_offset = add_off;
+  PDM_CHECK(pdm::layernorm_check(a));
+  PDM_HIP(pdm::layernorm_launch(a, c.s));
   return PDM_OK;
 }
 
@@ -340,7 +368,37 @@ int pdm_uvit_create(const pdm_uvit_cfg* cfg, pdm_uvit** out) {
 }
 
 int pdm_uvit_destroy(pdm_uvit* h) {
+  if (h)
+    for (auto e : h->prof_ev) (void)hipEventDestroy(e);
   delete h;
+  return PDM_OK;
+}
+
+int pdm_uvit_profile(pdm_uvit* h, int max_launches) {
+  if (!h || max_launches < 0) return fail(PDM_ERR_ARG, "pdm_uvit_profile: bad argument");
+  if (max_launches == 0) {
+    h->prof_on = false;
+    return PDM_OK;
+  }
+  while ((int)h->prof_ev.size() < 2 * max_launches) {
+    hipEvent_t e;
+    PDM_HIP(hipEventCreate(&e));
+    h->prof_ev.push_back(e);
+  }
+  h->prof_flops.assign(max_launches, 0.0);
+  h->prof_n = 0;
+  h->prof_on = true;
+  return PDM_OK;
+}
+
+int pdm_uvit_profile_read(pdm_uvit* h, float* ms, double* flops, int cap, int* n) {
+  if (!h || !n) return fail(PDM_ERR_ARG, "pdm_uvit_profile_read: bad argument");
+  *n = h->prof_n;
+  for (int i = 0; i < h->prof_n && i < cap; ++i) {
+    PDM_HIP(hipEventSynchronize(h->prof_ev[2 * i + 1]));
+    PDM_HIP(hipEventElapsedTime(&ms[i], h->prof_ev[2 * i], h->prof_ev[2 * i + 1]));
+    flops[i] = h->prof_flops[i];
+  }
   return PDM_OK;
 }
 
@@ -387,6 +445,7 @@ int pdm_uvit_forward(pdm_uvit* h, const float* x, const float* t, const int64_t*
   PDM_TRY(check_ready(h));
   Workspace w = layout(h, rows, (char*)workspace);
   if (w.bytes > workspace_bytes) return fail(PDM_ERR_ARG, "pdm_uvit_forward: workspace too small");
+  h->prof_n = 0;
   Ctx c{h, (hipStream_t)stream};
   const int D = h->D, L = h->Lx;
   {
@@ -413,16 +472,107 @@ int pdm_uvit_forward(pdm_uvit* h, const float* x, const float* t, const int64_t*
     const bf16* sk = h->cfg.skip ? w.SK + (h->nhalf - 1 - i) * MD : nullptr;
     PDM_TRY(run_block(c, "out_blocks." + std::to_string(i), w.X, rows, L, w.XB, sk, w.XB, w));
   }
-  PDM_TRY(run_head(c, w, rows, w.X, L, h->extras, "norm", "decoder_pred", h->C, h->P, h->P_pad, eps_pre, true));
+  PDM_TRY(final_norm(c, w, rows, w.X, L));
+  PDM_TRY(run_head(c, w.HEADIN, h->n_patch, 0, rows, "decoder_pred", h->C, h->P, h->P_pad, eps_pre));
   return PDM_OK;
 }
 
 int pdm_uvit_t2i_forward(pdm_uvit* h, const float* x, const float* t, const float* context, const float* mask_token,
                          int use_ground_truth, float* eps_pre, float* mask_pre, int rows, void* workspace,
                          size_t workspace_bytes, void* stream) {
-  (void)h; (void)x; (void)t; (void)context; (void)mask_token; (void)use_ground_truth; (void)eps_pre;
-  (void)mask_pre; (void)rows; (void)workspace; (void)workspace_bytes; (void)stream;
-  return fail(PDM_ERR_STATE, "pdm_uvit_t2i_forward: not built yet");
+  if (!h || !x || !t || !context || !eps_pre || rows <= 0) return fail(PDM_ERR_ARG, "pdm_uvit_t2i_forward: bad argument");
+  if (!h->cfg.t2i) return fail(PDM_ERR_ARG, "pdm_uvit_t2i_forward: not a t2i network");
+  const bool two = mask_token && h->cfg.separate && h->cfg.enable_panoptic;
+  if (mask_token && !two) return fail(PDM_ERR_ARG, "pdm_uvit_t2i_forward: mask tokens need enable_panoptic and separate");
+  if (two && !use_ground_truth && !mask_pre) return fail(PDM_ERR_ARG, "pdm_uvit_t2i_forward: mask_pre output missing");
+  PDM_TRY(check_ready(h));
+  Workspace w = layout(h, rows, (char*)workspace);
+  if (w.bytes > workspace_bytes) return fail(PDM_ERR_ARG, "pdm_uvit_t2i_forward: workspace too small");
+  h->prof_n = 0;
+  Ctx c{h, (hipStream_t)stream};
+  const int D = h->D, Lx = h->Lx, Lm = h->Lm, nctx = h->cfg.num_clip_token;
+  // context_embed (libs/uvit_t2i.py:387): bf16 cast + GEMM (+bias) -> fp32 context tokens
+  PDM_HIP(pdm::cast_bf16_launch(context, w.CTXB, (long long)rows * nctx * h->cfg.clip_dim, c.s));
+  PDM_TRY(gemm(c, w.CTXB, h->cfg.clip_dim, h->w("context_embed.weight"), h->f("context_embed.bias"), rows * nctx, D,
+               h->cfg.clip_dim, pdm::EPI_F32, nullptr, 0, w.CTXF, D, 0));
+  {  // image stream tokens [time, context x nctx, patches] + pos_embed (401-405 / 408-409)
+    pdm::AssembleArgs a{};
+    a.img = x; a.C = h->C; a.Himg = h->cfg.img_size; a.Wimg = h->cfg.img_size; a.p = h->p;
+    a.patch_w = h->f("patch_embed.proj.weight"); a.patch_b = h->f("patch_embed.proj.bias");
+    a.t = t; a.ctx_tokens = w.CTXF; a.n_ctx = nctx;
+    a.pos = h->f("pos_embed");
+    a.out = w.X; a.ld_out = D; a.B = rows; a.D = D; a.L_total = Lx;
+    a.row0_patch = h->extras; a.time_row = 0; a.label_row = -1; a.ctx_row = 1;
+    PDM_CHECK(pdm::assemble_check(a));
+    PDM_HIP(pdm::assemble_launch(a, c.s));
+  }
+  const size_t MDx = (size_t)rows * Lx * D;
+  if (!two) {  // plain text-conditioned U-ViT (mask_token None: 407-410, 516-517)
+    for (int i = 0; i < h->nhalf; ++i)
+      PDM_TRY(run_block(c, "in_blocks." + std::to_string(i), w.X, rows, Lx, nullptr, nullptr, w.SK + i * MDx, w));
+    PDM_TRY(run_block(c, "mid_block", w.X, rows, Lx, nullptr, nullptr, w.XB, w));
+    for (int i = 0; i < h->nhalf; ++i) {
+      const bf16* sk = h->cfg.skip ? w.SK + (h->nhalf - 1 - i) * MDx : nullptr;
+      PDM_TRY(run_block(c, "out_blocks." + std::to_string(i), w.X, rows, Lx, w.XB, sk, w.XB, w));
+    }
+    PDM_TRY(final_norm(c, w, rows, w.X, Lx));
+    PDM_TRY(run_head(c, w.HEADIN, h->n_patch, 0, rows, "decoder_pred", h->C, h->P, h->P_pad, eps_pre));
+    return PDM_OK;
+  }
+  {  // mask tokens m = mask_embed(mask_token) + pos_embed_mask (390, 406), stored at MX[:, Lx:Lm]
+    pdm::AssembleArgs a{};
+    a.img = mask_token; a.C = h->K; a.Himg = h->cfg.img_size; a.Wimg = h->cfg.img_size; a.p = h->p;
+    a.patch_w = h->f("mask_embed.proj.weight"); a.patch_b = h->f("mask_embed.proj.bias");
+    a.pos = h->f("pos_embed_mask");
+    a.out = w.MX + (size_t)Lx * D; a.ld_out = D; a.B = rows; a.D = D; a.L_total = Lm;
+    a.row0_patch = 0; a.time_row = -1; a.label_row = -1; a.ctx_row = -1;
+    PDM_CHECK(pdm::assemble_check(a));
+    PDM_HIP(pdm::assemble_launch(a, c.s));
+  }
+  const size_t MDm = (size_t)rows * Lm * D;
+  // mx = cat(x, m): refresh the image half of the mask stream before every mask block (426, 443, 459)
+  auto refresh = [&]() -> int {
+    PDM_HIP(pdm::rowcopy_launch(w.MX, D, w.X, D, rows * Lx, D, Lx, Lm, Lx, c.s));
+    return PDM_OK;
+  };
+  // x += zeroconv_{2l+1}(mx[:, :Lx]) (435-436, 452-453, 470-472) from the bf16 copy of the mask block output;
+  // the epilogue also leaves the bf16 copy of the new x (the skip / next skip_linear operand) in xb
+  auto inject = [&](int layer, const bf16* mxb, bf16* xb) -> int {
+    const std::string zc = "zero_convs." + std::to_string(2 * layer + 1) + ".conv";
+    return gemm(c, mxb, D, h->w(zc + ".weight"), h->f(zc + ".bias"), rows * Lx, D, D, pdm::EPI_F32, xb, D, w.X, D, 1,
+                nullptr, 0, 0, Lx, Lm);
+  };
+  int layer = 0;
+  for (int i = 0; i < h->nhalf; ++i, ++layer) {
+    PDM_TRY(refresh());
+    PDM_TRY(run_block(c, "in_blocks." + std::to_string(i), w.X, rows, Lx, nullptr, nullptr, nullptr, w));
+    PDM_TRY(run_block(c, "in_blocks_mask." + std::to_string(i), w.MX, rows, Lm, nullptr, nullptr, w.SKM + i * MDm, w));
+    PDM_TRY(inject(layer, w.SKM + i * MDm, w.SK + i * MDx));
+  }
+  PDM_TRY(refresh());
+  PDM_TRY(run_block(c, "mid_block", w.X, rows, Lx, nullptr, nullptr, nullptr, w));
+  PDM_TRY(run_block(c, "mid_block_mask", w.MX, rows, Lm, nullptr, nullptr, w.MXB, w));
+  PDM_TRY(inject(layer, w.MXB, w.XB));
+  ++layer;
+  for (int i = 0; i < h->nhalf; ++i, ++layer) {
+    PDM_TRY(refresh());
+    const bf16* sk = h->cfg.skip ? w.SK + (h->nhalf - 1 - i) * MDx : nullptr;
+    PDM_TRY(run_block(c, "out_blocks." + std::to_string(i), w.X, rows, Lx, w.XB, sk, nullptr, w));
+    const bf16* skm = h->cfg.skip ? w.SKM + (h->nhalf - 1 - i) * MDm : nullptr;
+    if (skm) PDM_HIP(pdm::cast_bf16_launch(w.MX, w.MXIN, (long long)MDm, c.s));
+    PDM_TRY(run_block(c, "out_blocks_mask." + std::to_string(i), w.MX, rows, Lm, w.MXIN, skm, w.MXB, w));
+    PDM_TRY(inject(layer, w.MXB, w.XB));
+  }
+  // heads (477-519): noise from norm(x) patch tokens; mask head on the un-normalised m (= MX[:, Lx:])
+  if (use_ground_truth) {
+    PDM_TRY(final_norm(c, w, rows, w.X, Lx, w.MX, Lm, Lx));
+  } else {
+    PDM_TRY(final_norm(c, w, rows, w.X, Lx));
+    const bf16* mb = h->nhalf > 0 ? w.MXB : w.MXB;  // bf16 copy of the last mask block output
+    PDM_TRY(run_head(c, mb, Lm, Lx, rows, "decoder_pred_mask", h->K, h->PK, h->PK_pad, mask_pre));
+  }
+  PDM_TRY(run_head(c, w.HEADIN, h->n_patch, 0, rows, "decoder_pred", h->C, h->P, h->P_pad, eps_pre));
+  return PDM_OK;
 }
 
 int pdm_stage_epilogue(const pdm_stage_epilogue_args* a, void* stream) {
@@ -438,6 +588,8 @@ int pdm_stage_epilogue(const pdm_stage_epilogue_args* a, void* stream) {
   for (int i = 0; i < 6; ++i) { e.T[i] = a->T[i]; e.c[i] = a->c[i]; }
   e.cm = a->cm;
   e.x_out = a->x_out;
+  e.x_out2 = a->x_out2;
+  e.x_out3 = a->x_out3;
   PDM_CHECK(pdm::epilogue_check(e));
   PDM_HIP(pdm::epilogue_launch(e, (hipStream_t)stream));
   return PDM_OK;

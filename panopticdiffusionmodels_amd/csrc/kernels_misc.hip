@@ -44,11 +44,17 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs p) {
   const f32x4* gm = reinterpret_cast<const f32x4*>(p.gamma);
   const f32x4* bt = reinterpret_cast<const f32x4*>(p.beta);
   bf16x4* y = reinterpret_cast<bf16x4*>(p.y + (size_t)r * p.ldy);
+  const f32x4* ad = nullptr;
+  if (p.add) {
+    const int arow = (r / p.rows_per_group) * p.add_group_stride + p.add_row_offset + (r % p.rows_per_group);
+    ad = reinterpret_cast<const f32x4*>(p.add + (size_t)arow * p.add_ld);
+  }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int idx = lane + i * 64;
     if (idx < nv) {
-      const f32x4 o = (v[i] - mean) * rstd * gm[idx] + bt[idx];
+      f32x4 o = (v[i] - mean) * rstd * gm[idx] + bt[idx];
+      if (ad) o += ad[idx];
       y[idx] = to_bf16x4(o[0], o[1], o[2], o[3]);
     }
   }
@@ -143,7 +149,8 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs p) {
   if (tok0 >= rows) return;
   const int g = lane >> 4, col = lane & 15;
   int m = tok0 + col;
-  const int mc = m < rows ? m : rows - 1;
+  const int mc0 = m < rows ? m : rows - 1;
+  const int mc = (mc0 / N) * p.in_group_stride + p.in_row_offset + mc0 % N;
   const int NT = p.P_pad >> 4;
   f32x4 acc[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
                   f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -231,6 +238,8 @@ __global__ __launch_bounds__(256) void epilogue_kernel(EpilogueArgs p) {
       float acc = p.cm * m;
       for (int i = 0; i < p.n_terms; ++i) acc += p.c[i] * p.T[i][e];
       p.x_out[e] = acc;
+      if (p.x_out2) p.x_out2[e] = acc;
+      if (p.x_out3) p.x_out3[e] = acc;
     }
   }
 }

@@ -36,6 +36,8 @@ struct LayerNormArgs {
   int rows, D;
   int rows_per_group, group_stride, row_offset;   // row gather (final norm over patch tokens only)
   float eps;
+  const float* add;           // optional fp32 rows added after the affine (gathered like x, with add_* below)
+  int add_ld, add_group_stride, add_row_offset;
 };
 const char* layernorm_check(const LayerNormArgs& p);
 hipError_t layernorm_launch(const LayerNormArgs& p, hipStream_t stream);
@@ -78,7 +80,8 @@ hipError_t assemble_launch(const AssembleArgs& p, hipStream_t stream);
 // decoder_pred (D -> P = p*p*C, bias) on bf16 patch rows + unpatchify scatter to NCHW fp32
 // (libs/uvit.py:182,225-228 and unpatchify 46-51; column order (p1, p2, C)).
 struct HeadArgs {
-  const bf16* x; int ldx;     // [B*N, D] rows (already LayerNorm-ed), N = (H/p)*(W/p)
+  const bf16* x; int ldx;     // token (b, i) is row b * in_group_stride + in_row_offset + i, N = (H/p)*(W/p)
+  int in_group_stride, in_row_offset;
   const bf16* W;              // [P_pad][D] (rows >= P are zero)
   const float* bias;          // [P]
   float* out;                 // [B, C, H, W]
@@ -103,7 +106,7 @@ struct EpilogueArgs {
   const float* xin; float ax, ae;
   float* m_out;
   int n_terms; const float* T[6]; float c[6]; float cm;
-  float* x_out;
+  float* x_out; float* x_out2; float* x_out3;   // x_out2/3: optional duplicate destinations
 };
 const char* epilogue_check(const EpilogueArgs& p);
 hipError_t epilogue_launch(const EpilogueArgs& p, hipStream_t stream);
