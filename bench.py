@@ -26,7 +26,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from panopticdiffusionmodels_amd import configs, weights  # noqa: E402
+from panopticdiffusionmodels_amd import configs, parallel, weights  # noqa: E402
 from panopticdiffusionmodels_amd.libs.autoencoder import get_model  # noqa: E402
 from panopticdiffusionmodels_amd.sampler import ClassCondSampler  # noqa: E402
 from panopticdiffusionmodels_amd.utils import get_nnet  # noqa: E402
@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=64, help="images per GPU per step")
+    ap.add_argument("--batch", type=int, default=95,
+                    help="images per GPU per step (95: 2x95x258 token rows tile the 256-row GEMM tiles exactly)")
     ap.add_argument("--config", default="imagenet256_uvit_large")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
@@ -87,16 +88,16 @@ def main():
     nsteps = args.warmup + args.steps
     zs, ys = [], []
     zshape = full["z_shape"]
-    for s in range(nsteps):
-        g = torch.Generator().manual_seed(1234 + (s * world + rank))
-        zs.append(torch.randn(B, *zshape, generator=g).to(dev))
-        ys.append(torch.randint(0, 1000, (B,), generator=g).to(dev) if null_label is not None else None)
-    gathered = torch.empty(world * B, *zshape, device=dev) if world > 1 else None
+    for s in range(nsteps):   # step s covers global samples [s*world*B, (s+1)*world*B), this rank its shard
+        idx = [s * world * B + i for i in parallel.shard(world * B, world, rank)]
+        z, y = parallel.sample_inputs(idx, zshape, num_classes=1000 if null_label is not None else None)
+        zs.append(z.to(dev))
+        ys.append(y.to(dev) if y is not None else None)
 
     def one_step(s):
         z = sampler.sample(zs[s], ys[s])
         if world > 1:
-            dist.all_gather_into_tensor(gathered, z)
+            parallel.gather_latents(z)
         if ae is not None:
             img = ae.decode(z)
             return img

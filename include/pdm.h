@@ -36,7 +36,9 @@ extern "C" {
 
 const char* pdm_last_error(void);
 int pdm_version(void);
-int pdm_device_arch(char* buf, int len);   /* gcnArchName of the current device, e.g. "gfx950:sramecc+:xnack-" */
+int pdm_device_arch(char* buf, int len);
+/* GEMM tile policy (benchmarking / A-B): 0 = auto, 1 = 128x128 tile, 2 = 256x256 tile */
+int pdm_set_gemm_algo(int algo);   /* gcnArchName of the current device, e.g. "gfx950:sramecc+:xnack-" */
 
 /* ---- network handle: libs/uvit.py:138-230 UViT, libs/uvit_t2i.py:258-525 UViT (t2i) -------------- */
 typedef struct pdm_uvit pdm_uvit;

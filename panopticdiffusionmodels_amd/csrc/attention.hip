@@ -36,8 +36,16 @@ __global__ __launch_bounds__(256) void attention_kernel(AttentionArgs p, int nqt
   __shared__ __attribute__((aligned(16))) char Vs[KC * VSTR];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int qt = blockIdx.x * 4 + wave;
+  // 1-D grid; blocks b and b+8 share an XCD (round-robin dispatch, placement affects speed only): give
+  // every query block of one (b, h) the same bid % 8 so its K/V chunks are re-read from that XCD's L2.
+  const int nqb = (nqt + 3) / 4;
+  const int bid = blockIdx.x;
+  const int grp = bid / (8 * nqb), rem = bid % (8 * nqb);
+  const int bh = grp * 8 + (rem & 7);
+  const int qb = rem >> 3;
+  if (bh >= p.B * p.H) return;
+  const int b = bh / p.H, h = bh % p.H;
+  const int qt = qb * 4 + wave;
   const bool active = qt < nqt;
   const int L = p.L, D = p.H * DH;
   const bf16* base = p.qkv + (size_t)b * L * p.ldq;
@@ -197,7 +205,9 @@ const char* attention_check(const AttentionArgs& p) {
 
 hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream) {
   const int nqt = (p.L + 15) / 16;
-  dim3 grid((nqt + 3) / 4, p.H, p.B), block(256);
+  const int nqb = (nqt + 3) / 4;
+  const int nbh = p.B * p.H;
+  dim3 grid(((nbh + 7) / 8) * 8 * nqb), block(256);
   switch (p.Dh) {
     case 32: hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, stream, p, nqt); break;
     case 64: hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, stream, p, nqt); break;

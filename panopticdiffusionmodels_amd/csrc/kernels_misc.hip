@@ -67,6 +67,26 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs p) {
 constexpr int ASM_TOK = 16;
 constexpr int ASM_MAXK = 64;
 
+template <int K>
+__device__ __forceinline__ void assemble_patches(const AssembleArgs& p, float* out, const float (*patch)[ASM_MAXK],
+                                                 int i0, int ntok) {
+  const int D = p.D;
+  for (int d = threadIdx.x; d < D; d += 256) {
+    float w[K];
+    const float* wr = p.patch_w + (size_t)d * K;
+#pragma unroll
+    for (int k = 0; k < K; ++k) w[k] = wr[k];
+    const float bias = p.patch_b[d];
+    for (int tk = 0; tk < ntok; ++tk) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc = fmaf(w[k], patch[tk][k], acc);
+      const int row = p.row0_patch + i0 + tk;
+      out[(size_t)row * p.ld_out + d] = acc + bias + p.pos[(size_t)row * D + d];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void assemble_kernel(AssembleArgs p) {
   const int b = blockIdx.y;
   const int D = p.D;
@@ -123,17 +143,21 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleArgs p) {
   }
   __syncthreads();
   const int ntok = min(ASM_TOK, n_patch - i0);
-  for (int d = threadIdx.x; d < D; d += 256) {
-    float w[ASM_MAXK];
-    const float* wr = p.patch_w + (size_t)d * K;
-    for (int k = 0; k < K; ++k) w[k] = wr[k];
-    const float bias = p.patch_b[d];
-    for (int tk = 0; tk < ntok; ++tk) {
-      float acc = 0.f;
-      for (int k = 0; k < K; ++k) acc = fmaf(w[k], patch[tk][k], acc);
-      const int row = p.row0_patch + i0 + tk;
-      out[(size_t)row * p.ld_out + d] = acc + bias + p.pos[(size_t)row * D + d];
-    }
+  switch (K) {  // C * p * p of the configs: 12 (CIFAR), 16 (L/2, H/2, t2i image), 32 (t2i mask), 64 (H/4)
+    case 12: assemble_patches<12>(p, out, patch, i0, ntok); break;
+    case 16: assemble_patches<16>(p, out, patch, i0, ntok); break;
+    case 32: assemble_patches<32>(p, out, patch, i0, ntok); break;
+    case 64: assemble_patches<64>(p, out, patch, i0, ntok); break;
+    default:
+      for (int d = threadIdx.x; d < D; d += 256) {
+        const float* wr = p.patch_w + (size_t)d * K;
+        for (int tk = 0; tk < ntok; ++tk) {
+          float acc = 0.f;
+          for (int k = 0; k < K; ++k) acc = fmaf(wr[k], patch[tk][k], acc);
+          const int row = p.row0_patch + i0 + tk;
+          out[(size_t)row * p.ld_out + d] = acc + p.patch_b[d] + p.pos[(size_t)row * D + d];
+        }
+      }
   }
 }
 

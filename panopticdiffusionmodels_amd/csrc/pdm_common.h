@@ -23,8 +23,23 @@ __device__ __forceinline__ void glds16(const void* gptr, PDM_LDS void* lds_wave_
   __builtin_amdgcn_global_load_lds(gptr, lds_wave_base, 16, 0, 0);
 }
 
+// erf(x) to |err| <= 1.5e-7 (Abramowitz & Stegun 7.1.26): one rcp, one exp, five FMAs, no branches --
+// far below the bf16 rounding (3.9e-3) of the GEMM outputs it feeds.
+__device__ __forceinline__ float erf_fast(float x) {
+  const float a = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
+  float y = fmaf(1.061405429f, t, -1.453152027f);
+  y = fmaf(y, t, 1.421413741f);
+  y = fmaf(y, t, -0.284496736f);
+  y = fmaf(y, t, 0.254829592f);
+  y *= t;
+  const float r = 1.0f - y * __expf(-a * a);
+  return copysignf(r, x);
+}
+
+// nn.GELU() default (exact erf form), libs/uvit.py:98 / libs/timm.py:102
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+  return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752440f));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

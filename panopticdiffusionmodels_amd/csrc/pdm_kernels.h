@@ -26,6 +26,7 @@ struct GemmArgs {
 
 const char* gemm_check(const GemmArgs& p, int epi);
 hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream);
+void gemm_set_algo(int algo);
 
 // LayerNorm over the last dim of fp32 rows -> bf16.  Row r of the output is row
 // (r / rows_per_group) * group_stride + row_offset + (r % rows_per_group) of the input.

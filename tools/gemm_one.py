@@ -1,0 +1,25 @@
+"""Run one GEMM shape repeatedly (profiling target): python tools/gemm_one.py ALGO M N K EPI [ITERS]"""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from panopticdiffusionmodels_amd import _lib  # noqa: E402
+
+algo, M, N, K, epi = (int(v) for v in sys.argv[1:6])
+iters = int(sys.argv[6]) if len(sys.argv) > 6 else 20
+lib = _lib.load()
+lib.pdm_set_gemm_algo(algo)
+g = torch.Generator(device="cuda").manual_seed(0)
+a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+b = torch.randn(N, device="cuda", generator=g)
+out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+of = torch.zeros(M, N, device="cuda")
+for _ in range(iters):
+    if epi == 2:
+        _lib.gemm(a, w, b, epi, out_f32=of, accumulate=True)
+    else:
+        _lib.gemm(a, w, b, epi, out=out)
+torch.cuda.synchronize()
+print("done")
