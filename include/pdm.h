@@ -131,6 +131,38 @@ int pdm_attention(const void* qkv, int ldq, void* out, int ldo, int B, int L, in
 /* fp32 -> bf16 conversion */
 int pdm_f32_to_bf16(const float* x, void* y, long long n, void* stream);
 
+/* ---------------------------------------------------------------------------------------------------
+ * KL-f8 decoder: FrozenAutoencoderKL.decode (libs/autoencoder.py:446-450) = z / scale_factor ->
+ * post_quant_conv -> Decoder.forward (libs/autoencoder.py:303-409).  Weights are registered under the
+ * reference state_dict keys with these repacks (done by libs/autoencoder.py on the Python side):
+ *   3x3 convs (except decoder.conv_in): bf16 [Cout][3][3][Cin]   (ky, kx, ci order)
+ *   decoder.conv_out: as above, padded to 4 output rows (bias padded to 4)
+ *   mid.attn_1.{q,k,v}: packed into "decoder.mid.attn_1.qkv.weight" bf16 [3C][C] + ".qkv.bias" f32 [3C]
+ *   proj_out / nin_shortcut (1x1): bf16 [Cout][Cin]
+ *   post_quant_conv, decoder.conv_in, norms, biases: fp32 in the reference layout
+ * Input z: fp32 [B, 4, h, w] (NCHW); output: fp32 [B, out_ch, 8h, 8w] (NCHW), not clamped. */
+typedef struct pdm_decoder pdm_decoder;
+
+typedef struct pdm_decoder_cfg {
+  int ch;              /* 128 */
+  int ch_mult[4];      /* (1, 2, 4, 4) */
+  int num_levels;      /* len(ch_mult) */
+  int num_res_blocks;  /* 2 (the up path runs num_res_blocks + 1 blocks per level) */
+  int z_channels;      /* 4 */
+  int out_ch;          /* 3 */
+  int latent_size;     /* h = w of z: 32 (256x256 images) or 64 (512x512) */
+  float scale_factor;  /* 0.18215 (libs/autoencoder.py:419) */
+} pdm_decoder_cfg;
+
+int pdm_decoder_create(const pdm_decoder_cfg* cfg, pdm_decoder** out);
+int pdm_decoder_destroy(pdm_decoder* d);
+int pdm_decoder_param_count(const pdm_decoder* d);
+int pdm_decoder_param_info(const pdm_decoder* d, int i, char* name, int len, int* dtype, long long* numel);
+int pdm_decoder_set_param(pdm_decoder* d, const char* name, const void* dev_ptr, int dtype, long long numel);
+int pdm_decoder_workspace_size(const pdm_decoder* d, int batch, size_t* bytes);
+int pdm_decoder_decode(pdm_decoder* d, const float* z, float* img, int batch, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

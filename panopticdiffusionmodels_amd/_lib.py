@@ -23,6 +23,12 @@ class PdmUvitCfg(ctypes.Structure):
         "enable_panoptic", "num_panoptic_class")]
 
 
+class PdmDecoderCfg(ctypes.Structure):
+    _fields_ = [("ch", ctypes.c_int), ("ch_mult", ctypes.c_int * 4), ("num_levels", ctypes.c_int),
+                ("num_res_blocks", ctypes.c_int), ("z_channels", ctypes.c_int), ("out_ch", ctypes.c_int),
+                ("latent_size", ctypes.c_int), ("scale_factor", ctypes.c_float)]
+
+
 class PdmStageEpilogueArgs(ctypes.Structure):
     _fields_ = [
         ("pre", ctypes.c_void_p), ("conv_w", ctypes.c_void_p), ("conv_b", ctypes.c_void_p),
@@ -72,6 +78,16 @@ _SIGS = {
     "pdm_attention": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p]),
     "pdm_f32_to_bf16": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]),
+    "pdm_decoder_create": (ctypes.c_int, [ctypes.POINTER(PdmDecoderCfg), ctypes.POINTER(ctypes.c_void_p)]),
+    "pdm_decoder_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "pdm_decoder_param_count": (ctypes.c_int, [ctypes.c_void_p]),
+    "pdm_decoder_param_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_longlong)]),
+    "pdm_decoder_set_param": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int,
+                                             ctypes.c_longlong]),
+    "pdm_decoder_workspace_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
+    "pdm_decoder_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

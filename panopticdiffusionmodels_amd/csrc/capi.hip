@@ -25,6 +25,14 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+}  // namespace
+
+namespace pdm {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace pdm
+
+namespace {
+
 #define PDM_HIP(call)                                                                   \
   do {                                                                                  \
     hipError_t e_ = (call);                                                             \
@@ -282,7 +290,7 @@ const char* pdm_last_error(void) { return g_err.c_str(); }
 int pdm_version(void) { return 1; }
 
 int pdm_set_gemm_algo(int algo) {
-  if (algo < 0 || algo > 3) return fail(PDM_ERR_ARG, "pdm_set_gemm_algo: algo must be 0 (auto), 1, 2 or 3");
+  if (algo < 0 || algo > 4) return fail(PDM_ERR_ARG, "pdm_set_gemm_algo: algo must be 0 (auto), 1, 2, 3 or 4");
   pdm::gemm_set_algo(algo);
   return PDM_OK;
 }

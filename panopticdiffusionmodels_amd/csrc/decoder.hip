@@ -1,0 +1,566 @@
+// KL-f8 decoder (libs/autoencoder.py:303-409 + FrozenAutoencoderKL.decode 446-450) on gfx950.
+//
+// Activations are NHWC; the residual stream is fp32, every conv input is a bf16 NHWC tensor produced by a
+// fused GroupNorm(32)+swish apply (or a plain cast).  Every 3x3 conv is an implicit GEMM on the U-ViT GEMM
+// kernels (conv mode: per-row tap addressing, padded taps read a zero page, the nearest-x2 upsample folded
+// into the source address), with bias and the residual add fused into the epilogue (EPI_F32 accumulate
+// into the residual stream).  The mid attention block (single head over h*w tokens, C = 512) runs as a
+// packed qkv GEMM, batched Q K^T / P V GEMMs and a row softmax.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/pdm.h"
+#include "pdm_common.h"
+#include "pdm_kernels.h"
+
+using pdm::bf16;
+
+namespace pdm {
+namespace {
+
+// ---------------------------------------------------------------------------------------------------
+// GroupNorm statistics: grid (nchunk, B); each block reduces PIX pixels x C channels in fp64 (sum, sumsq)
+// per group, partials -> [B, nchunk, 32, 2]; gn_final combines them into (mean, rstd) per (b, g).
+constexpr int GN_PIX = 64;
+
+template <typename T>
+__global__ __launch_bounds__(256) void gn_partial_kernel(const T* x, int P, int C, int nchunk, double* part) {
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const int cpg = C / 32;
+  __shared__ double s_sum[32], s_sq[32];
+  if (threadIdx.x < 32) { s_sum[threadIdx.x] = 0.0; s_sq[threadIdx.x] = 0.0; }
+  __syncthreads();
+  const int p0 = chunk * GN_PIX;
+  const int p1 = min(P, p0 + GN_PIX);
+  const T* xb = x + (size_t)b * P * C;
+  // thread -> 4 consecutive channels; lanes stride over channels, then pixels
+  const int nq = C / 4;
+  double su[2] = {0.0, 0.0}, sq[2] = {0.0, 0.0};
+  int gsel[2] = {-1, -1};
+  for (int q = threadIdx.x % nq, k = 0; k < 2 && q < nq; q += 256, ++k) gsel[k] = (q * 4) / cpg;
+  const int plane = threadIdx.x / nq;          // pixel lane (C < 1024)
+  const int planes = max(1, 256 / nq);
+  for (int pi = p0 + plane; pi < p1; pi += planes) {
+    const T* row = xb + (size_t)pi * C;
+    int k = 0;
+    for (int q = threadIdx.x % nq; q < nq && k < 2; q += 256, ++k) {
+      float v[4];
+      if constexpr (sizeof(T) == 4) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(row + q * 4);
+        v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+      } else {
+        const bf16x4 t = *reinterpret_cast<const bf16x4*>(row + q * 4);
+        v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
+      }
+      const float s4 = (v[0] + v[1]) + (v[2] + v[3]);
+      const float q4 = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+      su[k] += s4;
+      sq[k] += q4;
+    }
+  }
+  for (int k = 0; k < 2; ++k)
+    if (gsel[k] >= 0 && threadIdx.x < nq * planes) {
+      atomicAdd(&s_sum[gsel[k]], su[k]);
+      atomicAdd(&s_sq[gsel[k]], sq[k]);
+    }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    double* o = part + (((size_t)b * nchunk + chunk) * 32 + threadIdx.x) * 2;
+    o[0] = s_sum[threadIdx.x];
+    o[1] = s_sq[threadIdx.x];
+  }
+}
+
+__global__ __launch_bounds__(256) void gn_final_kernel(const double* part, int nchunk, double count, float eps,
+                                                       float* stats, int B) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // (b, g)
+  if (i >= B * 32) return;
+  const int b = i / 32, g = i % 32;
+  double s = 0.0, q = 0.0;
+  for (int c = 0; c < nchunk; ++c) {
+    const double* o = part + (((size_t)b * nchunk + c) * 32 + g) * 2;
+    s += o[0];
+    q += o[1];
+  }
+  const double mean = s / count;
+  double var = q / count - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  stats[i * 2] = (float)mean;
+  stats[i * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// y = [swish]((x - mean) * rstd * gamma + beta), NHWC, 4 channels per thread, bf16 out
+template <typename T>
+__global__ __launch_bounds__(256) void gn_apply_kernel(const T* x, const float* stats, const float* gamma,
+                                                       const float* beta, bf16* y, long long P, int C, int swish,
+                                                       int B) {
+  const int nq = C / 4;
+  const long long total = (long long)B * P * nq;
+  const int cpg = C / 32;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int q = (int)(e % nq);
+    const long long pix = e / nq;
+    const int b = (int)(pix / P);
+    const int c = q * 4;
+    const int g = c / cpg;
+    const float mean = stats[(b * 32 + g) * 2], rstd = stats[(b * 32 + g) * 2 + 1];
+    float v[4];
+    if constexpr (sizeof(T) == 4) {
+      const f32x4 t = *reinterpret_cast<const f32x4*>(x + pix * C + c);
+      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    } else {
+      const bf16x4 t = *reinterpret_cast<const bf16x4*>(x + pix * C + c);
+      v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
+    }
+    bf16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float u = (v[j] - mean) * rstd * gamma[c + j] + beta[c + j];
+      if (swish) u = u / (1.0f + __expf(-u));
+      o[j] = (bf16)u;
+    }
+    *reinterpret_cast<bf16x4*>(y + pix * C + c) = o;
+  }
+}
+
+// z [B, 4, h, w] fp32 -> z / scale -> post_quant_conv (1x1, 4->4) -> conv_in (3x3, 4->Cout) -> NHWC fp32
+__global__ __launch_bounds__(256) void conv_in_kernel(const float* z, float inv_scale, const float* pq_w,
+                                                      const float* pq_b, const float* w, const float* bias,
+                                                      float* out, int h, int wd, int Cout) {
+  const int b = blockIdx.y, y = blockIdx.x;
+  __shared__ float rows[3][4][66];   // 3 input rows x 4 channels x (w + 2 halo), post_quant applied
+  for (int e = threadIdx.x; e < 3 * 4 * (wd + 2); e += 256) {
+    const int r = e / (4 * (wd + 2)), rem = e % (4 * (wd + 2)), c = rem / (wd + 2), xx = rem % (wd + 2) - 1;
+    const int yy = y + r - 1;
+    float v = 0.f;
+    if (yy >= 0 && yy < h && xx >= 0 && xx < wd) {
+      v = pq_b[c];
+      for (int ci = 0; ci < 4; ++ci) v += pq_w[c * 4 + ci] * z[(((size_t)b * 4 + ci) * h + yy) * wd + xx] * inv_scale;
+    }
+    rows[r][c][xx + 1] = v;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < wd * Cout; e += 256) {
+    const int x = e / Cout, co = e % Cout;
+    float acc = bias[co];
+    const float* wp = w + (size_t)co * 36;
+    for (int ci = 0; ci < 4; ++ci)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) acc = fmaf(wp[ci * 9 + ky * 3 + kx], rows[ky][ci][x + kx], acc);
+    out[(((size_t)b * h + y) * wd + x) * Cout + co] = acc;
+  }
+}
+
+// row softmax of fp32 scores * scale -> bf16 probabilities (rows of n <= 4096), one block per row
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const float* s, bf16* p, int n, float scale) {
+  const float* row = s + (size_t)blockIdx.x * n;
+  bf16* out = p + (size_t)blockIdx.x * n;
+  __shared__ float red[8];
+  float m = -3.0e38f;
+  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, row[i] * scale);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) sum += __expf(row[i] * scale - m);
+  sum = wave_sum(sum);
+  if ((threadIdx.x & 63) == 0) red[4 + (threadIdx.x >> 6)] = sum;
+  __syncthreads();
+  const float inv = 1.0f / ((red[4] + red[5]) + (red[6] + red[7]));
+  for (int i = threadIdx.x; i < n; i += 256) out[i] = (bf16)(__expf(row[i] * scale - m) * inv);
+}
+
+// [B][n][ld] column block -> [B][C][n] transpose (bf16), 32x32 tiles through LDS
+__global__ __launch_bounds__(256) void transpose_kernel(const bf16* src, int ld, int col0, bf16* dst, int n, int C) {
+  __shared__ bf16 t[32][33];
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  const bf16* s = src + (size_t)b * n * ld + col0;
+  bf16* d = dst + (size_t)b * C * n;
+  for (int i = threadIdx.x; i < 1024; i += 256) {
+    const int r = i / 32, c = i % 32;
+    t[r][c] = s[(size_t)(r0 + r) * ld + c0 + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 1024; i += 256) {
+    const int c = i / 32, r = i % 32;
+    d[(size_t)(c0 + c) * n + r0 + r] = t[r][c];
+  }
+}
+
+// [B, HW, ldc] fp32 (first C channels) -> [B, C, H, W] fp32
+__global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(const float* in, int ldc, float* out, int HW, int C,
+                                                           int B) {
+  const long long total = (long long)B * C * HW;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int p = (int)(e % HW);
+    const long long bc = e / HW;
+    const int c = (int)(bc % C), b = (int)(bc / C);
+    out[e] = in[((size_t)b * HW + p) * ldc + c];
+  }
+}
+
+inline int gridn(long long n) {
+  long long g = (n + 255) / 256;
+  return (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+}  // namespace pdm
+
+// =====================================================================================================
+namespace {
+
+int dfail(int code, const std::string& m) { return pdm::set_error(code, m); }
+#define D_HIP(call)                                                                                   \
+  do {                                                                                                \
+    hipError_t e_ = (call);                                                                           \
+    if (e_ != hipSuccess) return dfail(PDM_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define D_CHECK(m)                              \
+  do {                                          \
+    const char* m_ = (m);                       \
+    if (m_) return dfail(PDM_ERR_ARG, m_);      \
+  } while (0)
+#define D_TRY(x)        \
+  do {                  \
+    int r_ = (x);       \
+    if (r_) return r_;  \
+  } while (0)
+
+struct DParam {
+  int dtype;
+  long long numel;
+  const void* ptr = nullptr;
+};
+
+}  // namespace
+
+struct pdm_decoder {
+  pdm_decoder_cfg cfg;
+  int nlev, top_ch, h0;
+  std::vector<std::string> order;
+  std::map<std::string, DParam> params;
+  void add(const std::string& n, int dt, long long ne) {
+    order.push_back(n);
+    params[n] = DParam{dt, ne, nullptr};
+  }
+  const float* f(const std::string& n) const { return (const float*)params.at(n).ptr; }
+  const bf16* w(const std::string& n) const { return (const bf16*)params.at(n).ptr; }
+  void add_res(const std::string& p, int cin, int cout) {
+    add(p + ".norm1.weight", PDM_F32, cin);
+    add(p + ".norm1.bias", PDM_F32, cin);
+    add(p + ".conv1.weight", PDM_BF16, 9LL * cin * cout);
+    add(p + ".conv1.bias", PDM_F32, cout);
+    add(p + ".norm2.weight", PDM_F32, cout);
+    add(p + ".norm2.bias", PDM_F32, cout);
+    add(p + ".conv2.weight", PDM_BF16, 9LL * cout * cout);
+    add(p + ".conv2.bias", PDM_F32, cout);
+    if (cin != cout) {
+      add(p + ".nin_shortcut.weight", PDM_BF16, 1LL * cin * cout);
+      add(p + ".nin_shortcut.bias", PDM_F32, cout);
+    }
+  }
+};
+
+namespace {
+
+struct DWork {
+  float* X;       // residual stream fp32 NHWC (max pixels x channels)
+  float* X2;      // second residual buffer (nin shortcut / upsample output)
+  bf16* G;        // bf16 conv input
+  bf16* H;        // bf16 conv1 output
+  bf16* QKV;      // attention: [B*hw, 3C]
+  float* S;       // attention scores [B, hw, hw]
+  bf16* P;        // probabilities [B, hw, hw]
+  bf16* VT;       // V^T [B, C, hw]
+  bf16* O;        // attention output [B*hw, C]
+  float* OUT4;    // conv_out [B*HW, 4]
+  double* part;   // GN partials
+  float* stats;   // GN (mean, rstd) [B, 32, 2]
+  bf16* zero;     // 256 zero bytes
+  size_t bytes;
+};
+
+size_t aup(size_t x) { return (x + 255) / 256 * 256; }
+using pdm::GN_PIX;
+
+DWork dlayout(const pdm_decoder* d, int B, char* base) {
+  DWork w{};
+  size_t off = 0;
+  auto take = [&](size_t n) {
+    char* p = base ? base + off : nullptr;
+    off = aup(off + n);
+    return p;
+  };
+  // largest activation: after the last upsample, 2^(nlev-1) * h0 squared pixels x the preceding level's C
+  size_t maxe = 0;
+  int res = d->h0, cin = d->top_ch;
+  for (int lvl = d->nlev - 1; lvl >= 0; --lvl) {
+    const int cout = d->cfg.ch * d->cfg.ch_mult[lvl];
+    size_t e = (size_t)res * res * (cin > cout ? cin : cout);
+    if (e > maxe) maxe = e;
+    cin = cout;
+    if (lvl != 0) {
+      res *= 2;
+      e = (size_t)res * res * cin;
+      if (e > maxe) maxe = e;
+    }
+  }
+  const size_t hw = (size_t)d->h0 * d->h0;
+  w.X = (float*)take((size_t)B * maxe * 4);
+  w.X2 = (float*)take((size_t)B * maxe * 4);
+  w.G = (bf16*)take((size_t)B * maxe * 2);
+  w.H = (bf16*)take((size_t)B * maxe * 2);
+  w.QKV = (bf16*)take((size_t)B * hw * 3 * d->top_ch * 2);
+  w.S = (float*)take((size_t)B * hw * hw * 4);
+  w.P = (bf16*)take((size_t)B * hw * hw * 2);
+  w.VT = (bf16*)take((size_t)B * hw * d->top_ch * 2);
+  w.O = (bf16*)take((size_t)B * hw * d->top_ch * 2);
+  w.OUT4 = (float*)take((size_t)B * res * res * 4 * 4);
+  w.part = (double*)take((size_t)B * ((size_t)res * res / GN_PIX + 1) * 32 * 2 * sizeof(double));
+  w.stats = (float*)take((size_t)B * 32 * 2 * 4);
+  w.zero = (bf16*)take(256);
+  w.bytes = off;
+  return w;
+}
+
+struct DCtx {
+  const pdm_decoder* d;
+  hipStream_t s;
+  const DWork* w;
+};
+
+template <typename T>
+int groupnorm(const DCtx& c, const T* x, int B, int P, int C, const std::string& norm, bf16* y, bool swish) {
+  const int nchunk = (P + pdm::GN_PIX - 1) / pdm::GN_PIX;
+  hipLaunchKernelGGL(pdm::gn_partial_kernel<T>, dim3(nchunk, B), dim3(256), 0, c.s, x, P, C, nchunk, c.w->part);
+  hipLaunchKernelGGL(pdm::gn_final_kernel, dim3((B * 32 + 255) / 256), dim3(256), 0, c.s, c.w->part, nchunk,
+                     (double)P * (C / 32), 1e-6f, c.w->stats, B);
+  const long long n = (long long)B * P * (C / 4);
+  hipLaunchKernelGGL(pdm::gn_apply_kernel<T>, dim3(pdm::gridn(n)), dim3(256), 0, c.s, x, c.w->stats,
+                     c.d->f(norm + ".weight"), c.d->f(norm + ".bias"), y, (long long)P, C, swish ? 1 : 0, B);
+  D_HIP(hipGetLastError());
+  return PDM_OK;
+}
+
+// implicit-GEMM conv3x3 (in: bf16 NHWC [B, res>>up, res>>up, cin]) -> epilogue
+int conv3(const DCtx& c, const bf16* in, int B, int res, int cin, int cout, const std::string& name, int epi,
+          bf16* ob, float* of, int accumulate, int up = 0) {
+  pdm::GemmArgs a{};
+  a.A1 = in; a.lda1 = cin; a.K1 = 9 * cin;
+  a.W = c.d->w(name + ".weight"); a.bias = c.d->f(name + ".bias");
+  a.M = B * res * res; a.N = cout; a.K = 9 * cin;
+  a.out_bf16 = ob; a.ldo = cout; a.out_f32 = of; a.ldr = cout; a.accumulate = accumulate;
+  a.conv = 1; a.convH = res; a.convW = res; a.convC = cin; a.conv_up = up; a.zero = c.w->zero;
+  D_CHECK(pdm::gemm_check(a, epi));
+  D_HIP(pdm::gemm_launch(a, epi, c.s));
+  return PDM_OK;
+}
+
+int linear(const DCtx& c, const bf16* A, int M, int K, const bf16* W, const float* bias, int N, int epi, bf16* ob,
+           float* of, int accumulate) {
+  pdm::GemmArgs a{};
+  a.A1 = A; a.lda1 = K; a.K1 = K; a.W = W; a.bias = bias; a.M = M; a.N = N; a.K = K;
+  a.out_bf16 = ob; a.ldo = N; a.out_f32 = of; a.ldr = N; a.accumulate = accumulate;
+  D_CHECK(pdm::gemm_check(a, epi));
+  D_HIP(pdm::gemm_launch(a, epi, c.s));
+  return PDM_OK;
+}
+
+// ResnetBlock (libs/autoencoder.py:75-134): X (fp32 NHWC, cin) -> X (cout) in place (or via X2 for nin)
+int resblock(const DCtx& c, float*& X, float*& X2, int B, int res, int cin, int cout, const std::string& p) {
+  const DWork& w = *c.w;
+  const int P = res * res;
+  D_TRY(groupnorm<float>(c, X, B, P, cin, p + ".norm1", w.G, true));
+  D_TRY(conv3(c, w.G, B, res, cin, cout, p + ".conv1", pdm::EPI_BF16, w.H, nullptr, 0));
+  D_TRY(groupnorm<bf16>(c, w.H, B, P, cout, p + ".norm2", w.G, true));
+  if (cin != cout) {
+    // x = nin_shortcut(x): 1x1 conv = GEMM on a bf16 copy of x, into X2; then X2 += conv2(h)
+    D_HIP(pdm::cast_bf16_launch(X, w.H, (long long)B * P * cin, c.s));
+    D_TRY(linear(c, w.H, B * P, cin, c.d->w(p + ".nin_shortcut.weight"), c.d->f(p + ".nin_shortcut.bias"), cout,
+                 pdm::EPI_F32, nullptr, X2, 0));
+    D_TRY(conv3(c, w.G, B, res, cout, cout, p + ".conv2", pdm::EPI_F32, nullptr, X2, 1));
+    float* t = X;
+    X = X2;
+    X2 = t;
+  } else {
+    D_TRY(conv3(c, w.G, B, res, cout, cout, p + ".conv2", pdm::EPI_F32, nullptr, X, 1));
+  }
+  return PDM_OK;
+}
+
+// AttnBlock (libs/autoencoder.py:143-195), single head over hw tokens, channels C
+int attnblock(const DCtx& c, float* X, int B, int res, int C, const std::string& p) {
+  const DWork& w = *c.w;
+  const int hw = res * res;
+  D_TRY(groupnorm<float>(c, X, B, hw, C, p + ".norm", w.G, false));
+  D_TRY(linear(c, w.G, B * hw, C, c.d->w(p + ".qkv.weight"), c.d->f(p + ".qkv.bias"), 3 * C, pdm::EPI_BF16, w.QKV,
+               nullptr, 0));
+  {  // S[b] = Q[b] K[b]^T  (batched over b)
+    pdm::GemmArgs a{};
+    a.A1 = w.QKV; a.lda1 = 3 * C; a.K1 = C;
+    a.W = w.QKV + C; a.ldw = 3 * C;
+    a.M = hw; a.N = hw; a.K = C;
+    a.out_f32 = w.S; a.ldr = hw;
+    a.batch = B; a.sA = (long long)hw * 3 * C; a.sW = (long long)hw * 3 * C; a.sR = (long long)hw * hw;
+    D_CHECK(pdm::gemm_check(a, pdm::EPI_F32));
+    D_HIP(pdm::gemm_launch(a, pdm::EPI_F32, c.s));
+  }
+  hipLaunchKernelGGL(pdm::softmax_rows_kernel, dim3(B * hw), dim3(256), 0, c.s, w.S, w.P, hw, 1.0f / sqrtf((float)C));
+  hipLaunchKernelGGL(pdm::transpose_kernel, dim3(hw / 32, C / 32, B), dim3(256), 0, c.s, w.QKV, 3 * C, 2 * C, w.VT, hw, C);
+  D_HIP(hipGetLastError());
+  {  // O[b] = P[b] V[b]  with V^T as the [N][K] operand
+    pdm::GemmArgs a{};
+    a.A1 = w.P; a.lda1 = hw; a.K1 = hw;
+    a.W = w.VT;
+    a.M = hw; a.N = C; a.K = hw;
+    a.out_bf16 = w.O; a.ldo = C;
+    a.batch = B; a.sA = (long long)hw * hw; a.sW = (long long)C * hw; a.sO = (long long)hw * C;
+    D_CHECK(pdm::gemm_check(a, pdm::EPI_BF16));
+    D_HIP(pdm::gemm_launch(a, pdm::EPI_BF16, c.s));
+  }
+  // x + proj_out(o)
+  D_TRY(linear(c, w.O, B * hw, C, c.d->w(p + ".proj_out.weight"), c.d->f(p + ".proj_out.bias"), C, pdm::EPI_F32,
+               nullptr, X, 1));
+  return PDM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pdm_decoder_create(const pdm_decoder_cfg* cfg, pdm_decoder** out) {
+  if (!cfg || !out) return dfail(PDM_ERR_ARG, "pdm_decoder_create: null argument");
+  const pdm_decoder_cfg& c = *cfg;
+  if (c.num_levels < 1 || c.num_levels > 4) return dfail(PDM_ERR_ARG, "decoder: 1..4 levels supported");
+  if (c.z_channels != 4) return dfail(PDM_ERR_ARG, "decoder: z_channels must be 4");
+  if (c.out_ch > 4) return dfail(PDM_ERR_ARG, "decoder: out_ch must be <= 4");
+  for (int i = 0; i < c.num_levels; ++i)
+    if ((c.ch * c.ch_mult[i]) % 64) return dfail(PDM_ERR_ARG, "decoder: channel counts must be multiples of 64");
+  if (c.latent_size % 8 || c.latent_size > 64) return dfail(PDM_ERR_ARG, "decoder: latent size must be a multiple of 8, <= 64");
+  pdm_decoder* d = new pdm_decoder();
+  d->cfg = c;
+  d->nlev = c.num_levels;
+  d->top_ch = c.ch * c.ch_mult[c.num_levels - 1];
+  d->h0 = c.latent_size;
+  const int T = d->top_ch;
+  d->add("post_quant_conv.weight", PDM_F32, 16);
+  d->add("post_quant_conv.bias", PDM_F32, 4);
+  d->add("decoder.conv_in.weight", PDM_F32, (long long)T * 36);
+  d->add("decoder.conv_in.bias", PDM_F32, T);
+  d->add_res("decoder.mid.block_1", T, T);
+  d->add("decoder.mid.attn_1.norm.weight", PDM_F32, T);
+  d->add("decoder.mid.attn_1.norm.bias", PDM_F32, T);
+  d->add("decoder.mid.attn_1.qkv.weight", PDM_BF16, 3LL * T * T);
+  d->add("decoder.mid.attn_1.qkv.bias", PDM_F32, 3LL * T);
+  d->add("decoder.mid.attn_1.proj_out.weight", PDM_BF16, 1LL * T * T);
+  d->add("decoder.mid.attn_1.proj_out.bias", PDM_F32, T);
+  d->add_res("decoder.mid.block_2", T, T);
+  int cin = T;
+  for (int lvl = d->nlev - 1; lvl >= 0; --lvl) {
+    const int cout = c.ch * c.ch_mult[lvl];
+    for (int b = 0; b <= c.num_res_blocks; ++b) {
+      d->add_res("decoder.up." + std::to_string(lvl) + ".block." + std::to_string(b), cin, cout);
+      cin = cout;
+    }
+    if (lvl != 0) {
+      d->add("decoder.up." + std::to_string(lvl) + ".upsample.conv.weight", PDM_BF16, 9LL * cin * cin);
+      d->add("decoder.up." + std::to_string(lvl) + ".upsample.conv.bias", PDM_F32, cin);
+    }
+  }
+  d->add("decoder.norm_out.weight", PDM_F32, cin);
+  d->add("decoder.norm_out.bias", PDM_F32, cin);
+  d->add("decoder.conv_out.weight", PDM_BF16, 4LL * 9 * cin);   // padded to 4 output rows
+  d->add("decoder.conv_out.bias", PDM_F32, 4);
+  *out = d;
+  return PDM_OK;
+}
+
+int pdm_decoder_destroy(pdm_decoder* d) {
+  delete d;
+  return PDM_OK;
+}
+
+int pdm_decoder_param_count(const pdm_decoder* d) { return d ? (int)d->order.size() : 0; }
+
+int pdm_decoder_param_info(const pdm_decoder* d, int i, char* name, int len, int* dtype, long long* numel) {
+  if (!d || i < 0 || i >= (int)d->order.size()) return dfail(PDM_ERR_ARG, "pdm_decoder_param_info: index out of range");
+  snprintf(name, len, "%s", d->order[i].c_str());
+  *dtype = d->params.at(d->order[i]).dtype;
+  *numel = d->params.at(d->order[i]).numel;
+  return PDM_OK;
+}
+
+int pdm_decoder_set_param(pdm_decoder* d, const char* name, const void* ptr, int dtype, long long numel) {
+  if (!d || !name) return dfail(PDM_ERR_ARG, "pdm_decoder_set_param: null argument");
+  auto it = d->params.find(name);
+  if (it == d->params.end()) return dfail(PDM_ERR_ARG, std::string("pdm_decoder_set_param: unexpected key ") + name);
+  if (it->second.dtype != dtype || it->second.numel != numel)
+    return dfail(PDM_ERR_ARG, std::string("pdm_decoder_set_param: dtype/size mismatch for ") + name);
+  if ((uintptr_t)ptr & 15) return dfail(PDM_ERR_ARG, std::string("pdm_decoder_set_param: unaligned ") + name);
+  it->second.ptr = ptr;
+  return PDM_OK;
+}
+
+int pdm_decoder_workspace_size(const pdm_decoder* d, int B, size_t* bytes) {
+  if (!d || B <= 0 || !bytes) return dfail(PDM_ERR_ARG, "pdm_decoder_workspace_size: bad argument");
+  *bytes = dlayout(d, B, nullptr).bytes;
+  return PDM_OK;
+}
+
+int pdm_decoder_decode(pdm_decoder* d, const float* z, float* img, int B, void* workspace, size_t workspace_bytes,
+                       void* stream) {
+  if (!d || !z || !img || B <= 0) return dfail(PDM_ERR_ARG, "pdm_decoder_decode: bad argument");
+  for (auto& n : d->order)
+    if (!d->params[n].ptr) return dfail(PDM_ERR_STATE, "pdm_decoder: weight not registered: " + n);
+  DWork w = dlayout(d, B, (char*)workspace);
+  if (w.bytes > workspace_bytes) return dfail(PDM_ERR_ARG, "pdm_decoder_decode: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  DCtx c{d, s, &w};
+  D_HIP(hipMemsetAsync(w.zero, 0, 256, s));
+  const int T = d->top_ch;
+  int res = d->h0;
+  float* X = w.X;
+  float* X2 = w.X2;
+  hipLaunchKernelGGL(pdm::conv_in_kernel, dim3(res, B), dim3(256), 0, s, z, 1.0f / d->cfg.scale_factor,
+                     d->f("post_quant_conv.weight"), d->f("post_quant_conv.bias"), d->f("decoder.conv_in.weight"),
+                     d->f("decoder.conv_in.bias"), X, res, res, T);
+  D_HIP(hipGetLastError());
+  D_TRY(resblock(c, X, X2, B, res, T, T, "decoder.mid.block_1"));
+  D_TRY(attnblock(c, X, B, res, T, "decoder.mid.attn_1"));
+  D_TRY(resblock(c, X, X2, B, res, T, T, "decoder.mid.block_2"));
+  int cin = T;
+  for (int lvl = d->nlev - 1; lvl >= 0; --lvl) {
+    const int cout = d->cfg.ch * d->cfg.ch_mult[lvl];
+    for (int b = 0; b <= d->cfg.num_res_blocks; ++b) {
+      D_TRY(resblock(c, X, X2, B, res, cin, cout, "decoder.up." + std::to_string(lvl) + ".block." + std::to_string(b)));
+      cin = cout;
+    }
+    if (lvl != 0) {  // nearest x2 upsample folded into the conv's source addressing (35-50)
+      D_HIP(pdm::cast_bf16_launch(X, w.G, (long long)B * res * res * cin, s));
+      res *= 2;
+      D_TRY(conv3(c, w.G, B, res, cin, cin, "decoder.up." + std::to_string(lvl) + ".upsample.conv", pdm::EPI_F32,
+                  nullptr, X2, 0, 1));
+      float* t = X;
+      X = X2;
+      X2 = t;
+    }
+  }
+  D_TRY(groupnorm<float>(c, X, B, res * res, cin, "decoder.norm_out", w.G, true));
+  D_TRY(conv3(c, w.G, B, res, cin, 4, "decoder.conv_out", pdm::EPI_F32, nullptr, w.OUT4, 0));
+  hipLaunchKernelGGL(pdm::nhwc_to_nchw_kernel, dim3(pdm::gridn((long long)B * d->cfg.out_ch * res * res)), dim3(256), 0,
+                     s, w.OUT4, 4, img, res * res, d->cfg.out_ch, B);
+  D_HIP(hipGetLastError());
+  return PDM_OK;
+}
+
+}  // extern "C"

@@ -18,6 +18,16 @@ namespace pdm {
 
 namespace {
 constexpr int BM = 128, BN = 128, BK = 64;
+
+// A-operand row pointer for k-columns [k0, k0 + 64): dense rows, or an implicit-GEMM conv3x3 tap.
+// (b, y, x) of the row's output pixel is passed in; returns the address of element k0 of that row.
+__device__ __forceinline__ const bf16* conv_row_ptr(const GemmArgs& p, const bf16* A1, int b, int y, int x, int k0) {
+  const int tap = k0 / p.convC, ci0 = k0 - tap * p.convC;
+  const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+  if (yy < 0 || yy >= p.convH || xx < 0 || xx >= p.convW) return p.zero;
+  const int sh = p.conv_up, Hs = p.convH >> sh, Ws = p.convW >> sh;
+  return A1 + (((size_t)b * Hs + (yy >> sh)) * Ws + (xx >> sh)) * p.convC + ci0;
+}
 constexpr int TILE_BYTES = BM * BK * 2;           // 16 KiB per operand tile
 constexpr int SMEM_BYTES = 2 * 2 * TILE_BYTES;    // 2 stages x (A, W)
 
@@ -41,6 +51,14 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p, int tiles
   }
   const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
+  if (p.batch > 1) {
+    const long long z = blockIdx.y;
+    p.A1 += z * p.sA;
+    p.W += z * p.sW;
+    if (p.out_bf16) p.out_bf16 += z * p.sO;
+    if (p.out_f32) p.out_f32 += z * p.sR;
+  }
+  const int ldw = p.ldw > 0 ? p.ldw : p.K;
 
   auto stage = [&](int kt, int buf) {
     const int k0 = kt * BK;
@@ -57,11 +75,18 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p, int tiles
       const int c = (lane & 7) ^ ((row >> 1) & 7);
       int gm = m0 + row;
       gm = gm < p.M ? gm : p.M - 1;
-      if (p.a_rows_per_group > 0 && k0 < p.K1) gm = (gm / p.a_rows_per_group) * p.a_group_stride + gm % p.a_rows_per_group;
-      glds16(Ab + (size_t)gm * lda + ka + c * 8, (PDM_LDS void*)(sa + rg * 1024));
+      const bf16* arow;
+      if (p.conv) {
+        const int hw = p.convH * p.convW, b = gm / hw, r = gm - b * hw;
+        arow = conv_row_ptr(p, Ab, b, r / p.convW, r % p.convW, ka);
+      } else {
+        if (p.a_rows_per_group > 0 && k0 < p.K1) gm = (gm / p.a_rows_per_group) * p.a_group_stride + gm % p.a_rows_per_group;
+        arow = Ab + (size_t)gm * lda + ka;
+      }
+      glds16(arow + c * 8, (PDM_LDS void*)(sa + rg * 1024));
       int gn = n0 + row;
       gn = gn < p.N ? gn : p.N - 1;
-      glds16(p.W + (size_t)gn * p.K + k0 + c * 8, (PDM_LDS void*)(sw + rg * 1024));
+      glds16(p.W + (size_t)gn * ldw + k0 + c * 8, (PDM_LDS void*)(sw + rg * 1024));
     }
   };
 
@@ -151,6 +176,168 @@ __device__ __forceinline__ void wait_vmcnt() {
   else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 }
 
+// Fragment f of a 256x256 tile's accumulators -> (row, column) of its 16x4 piece within the tile.
+//   MAP 0 (gemm256_kernel): wave (wm, wn) owns rows wm*128 + [0,128), columns wn*64 + [0,64); f = ni*8 + mi
+//   MAP 1 (gemm8p_kernel):  quadrant (qi, qj) of the tile, wave owns rows qi*128 + wm*64 + [0,64),
+//                            columns qj*128 + wn*32 + [0,32); f = ((qi*2 + qj)*2 + ni)*4 + mi
+template <int MAP>
+__device__ __forceinline__ void frag_pos(int f, int lane, int wm, int wn, int& ml, int& nl) {
+  if constexpr (MAP == 0) {
+    const int ni = f / 8, mi = f % 8;
+    ml = wm * 128 + mi * 16 + (lane & 15);
+    nl = wn * 64 + ni * 16 + (lane >> 4) * 4;
+  } else {
+    const int qi = f / 16, qj = (f / 8) & 1, ni = (f / 4) & 1, mi = f & 3;
+    ml = qi * 128 + wm * 64 + mi * 16 + (lane & 15);
+    nl = qj * 128 + wn * 32 + ni * 16 + (lane >> 4) * 4;
+  }
+}
+
+// Epilogue of a 256x256 tile (needs 128 KiB of LDS; the staging ring is free by then).
+//  bf16 / GELU: the bf16 tile is written to LDS with a row-XOR chunk swizzle, then stored row-contiguously
+//    with 16-byte stores (full lines, half the store instructions of the per-lane 8-byte scatter).
+//  fp32 residual: two 128-row passes through LDS; every thread then owns 8 consecutive columns of a row:
+//    2 x 16-byte residual loads, 2 x 16-byte stores and one 16-byte bf16 copy store per row chunk.
+template <int EPI, int MAP>
+__device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc)[32], char* smem, int m0, int n0,
+                                            int tid, int lane, int wm, int wn) {
+  // bias of the lane's 4 column groups, loaded up front with one wave-uniform branch (columns past N read a
+  // clamped address and are never stored)
+  f32x4 bv[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bv[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (EPI != EPI_F32 && p.bias) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      int ml, nl;
+      frag_pos<MAP>(MAP == 0 ? g * 8 : (g >> 1) * 8 + (g & 1) * 4, lane, wm, wn, ml, nl);
+      const int n = min(n0 + nl, p.N - 4);
+      bv[g] = *reinterpret_cast<const f32x4*>(p.bias + n);
+    }
+  }
+  const bool full = (m0 + 256 <= p.M) && (n0 + 256 <= p.N);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
+#pragma unroll
+    for (int f = 0; f < 32; ++f) {
+      int ml, nl;
+      frag_pos<MAP>(f, lane, wm, wn, ml, nl);
+      f32x4 v = acc[f] + bv[MAP == 0 ? f / 8 : (f / 8 & 1) * 2 + (f / 4 & 1)];
+      if constexpr (EPI == EPI_GELU) {
+        v[0] = gelu_erf(v[0]); v[1] = gelu_erf(v[1]); v[2] = gelu_erf(v[2]); v[3] = gelu_erf(v[3]);
+      }
+      const int off = ml * 512 + ((((nl >> 3) ^ (ml & 31)) << 4) | ((nl & 4) << 1));
+      *reinterpret_cast<bf16x4*>(smem + off) = to_bf16x4(v[0], v[1], v[2], v[3]);
+    }
+    __syncthreads();
+    i32x4 v[16];
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int idx = it * 512 + tid;
+      const int ml = idx >> 5, ch = idx & 31;
+      v[it] = *reinterpret_cast<const i32x4*>(smem + ml * 512 + ((ch ^ (ml & 31)) << 4));
+    }
+    if (full) {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int idx = it * 512 + tid;
+        *reinterpret_cast<i32x4*>(p.out_bf16 + (size_t)(m0 + (idx >> 5)) * p.ldo + n0 + (idx & 31) * 8) = v[it];
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int idx = it * 512 + tid;
+        const int m = m0 + (idx >> 5), n = n0 + (idx & 31) * 8;
+        if (m < p.M && n < p.N) *reinterpret_cast<i32x4*>(p.out_bf16 + (size_t)m * p.ldo + n) = v[it];
+      }
+    }
+    return;
+  }
+  // fp32: the thread's 8 store columns n0 + (tid & 31) * 8 are the same in every row it stores
+  f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  if (p.bias) {
+    const int n = min(n0 + (tid & 31) * 8, p.N - 8 >= 0 ? p.N - 8 : 0);
+    b0 = *reinterpret_cast<const f32x4*>(p.bias + n);
+    if (n + 4 < p.N) b1 = *reinterpret_cast<const f32x4*>(p.bias + n + 4);
+  }
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int f = 0; f < 32; ++f) {
+      int ml, nl;
+      frag_pos<MAP>(f, lane, wm, wn, ml, nl);
+      if ((ml >> 7) != pass) continue;   // compile-time for MAP 1; wave-uniform for MAP 0
+      ml &= 127;
+      *reinterpret_cast<f32x4*>(smem + ml * 1024 + (((nl >> 2) ^ (ml & 63)) << 4)) = acc[f];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      f32x4 v0[4], v1[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int idx = (g * 4 + i) * 512 + tid;
+        const int ml = idx >> 5, c8 = idx & 31;
+        v0[i] = *reinterpret_cast<const f32x4*>(smem + ml * 1024 + (((2 * c8) ^ (ml & 63)) << 4)) + b0;
+        v1[i] = *reinterpret_cast<const f32x4*>(smem + ml * 1024 + (((2 * c8 + 1) ^ (ml & 63)) << 4)) + b1;
+      }
+      if (full) {
+        if (p.accumulate) {
+          f32x4 r0[4], r1[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int idx = (g * 4 + i) * 512 + tid;
+            const f32x4* r = reinterpret_cast<const f32x4*>(p.out_f32 + (size_t)(m0 + pass * 128 + (idx >> 5)) * p.ldr + n0 + (idx & 31) * 8);
+            r0[i] = r[0];
+            r1[i] = r[1];
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) { v0[i] += r0[i]; v1[i] += r1[i]; }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int idx = (g * 4 + i) * 512 + tid;
+          const size_t m = m0 + pass * 128 + (idx >> 5);
+          const int n = n0 + (idx & 31) * 8;
+          f32x4* r = reinterpret_cast<f32x4*>(p.out_f32 + m * p.ldr + n);
+          r[0] = v0[i];
+          r[1] = v1[i];
+          if (p.out_bf16) {
+            bf16x8 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { o[j] = (bf16)v0[i][j]; o[4 + j] = (bf16)v1[i][j]; }
+            *reinterpret_cast<bf16x8*>(p.out_bf16 + m * p.ldo + n) = o;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int idx = (g * 4 + i) * 512 + tid;
+          const int m = m0 + pass * 128 + (idx >> 5), n = n0 + (idx & 31) * 8;
+          if (m < p.M && n < p.N) {
+            f32x4* r = reinterpret_cast<f32x4*>(p.out_f32 + (size_t)m * p.ldr + n);
+            f32x4 a = v0[i], b = v1[i];
+            if (p.accumulate) {
+              a += r[0];
+              b += r[1];
+            }
+            r[0] = a;
+            r[1] = b;
+            if (p.out_bf16) {
+              bf16x8 o;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) { o[j] = (bf16)a[j]; o[4 + j] = (bf16)b[j]; }
+              *reinterpret_cast<bf16x8*>(p.out_bf16 + (size_t)m * p.ldo + n) = o;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <int EPI, int BK, int NS>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs p, int tiles_n, int nwg) {
   constexpr int ROWB = BK * 2;                 // bytes per LDS row
@@ -169,6 +356,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs p, int tiles_n
   }
   const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
   const int m0 = tm * BM2, n0 = tn * BN2;
+  if (p.batch > 1) {
+    const long long z = blockIdx.y;
+    p.A1 += z * p.sA;
+    p.W += z * p.sW;
+    if (p.out_bf16) p.out_bf16 += z * p.sO;
+    if (p.out_f32) p.out_f32 += z * p.sR;
+  }
+  const int ldw = p.ldw > 0 ? p.ldw : p.K;
 
   const int prow = lane / CPR;
   const int pch = lane % CPR;
@@ -176,6 +371,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs p, int tiles_n
   const bf16* a2src[PPW];
   const bf16* wsrc[PPW];
   int soff[PPW];
+  int cb[PPW], cy[PPW], cx[PPW];   // conv mode: output pixel of each piece row
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
     const int row = (wave * PPW + i) * RPP + prow;
@@ -186,9 +382,16 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs p, int tiles_n
     const int gm1 = p.a_rows_per_group > 0 ? (gm / p.a_rows_per_group) * p.a_group_stride + gm % p.a_rows_per_group : gm;
     asrc[i] = p.A1 + (size_t)gm1 * p.lda1;
     a2src[i] = p.A2 ? p.A2 + (size_t)gm * p.lda2 : nullptr;
+    if (p.conv) {
+      const int hw = p.convH * p.convW;
+      cb[i] = gm / hw;
+      const int r = gm - cb[i] * hw;
+      cy[i] = r / p.convW;
+      cx[i] = r - cy[i] * p.convW;
+    }
     int gn = n0 + row;
     gn = gn < p.N ? gn : p.N - 1;
-    wsrc[i] = p.W + (size_t)gn * p.K;
+    wsrc[i] = p.W + (size_t)gn * ldw;
   }
 
   auto issue = [&](int j) {
@@ -197,7 +400,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs p, int tiles_n
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int piece = wave * PPW + i;
-      const bf16* src = (k0 < p.K1) ? asrc[i] + k0 + soff[i] : a2src[i] + (k0 - p.K1) + soff[i];
+      const bf16* src;
+      if (p.conv) src = conv_row_ptr(p, p.A1, cb[i], cy[i], cx[i], k0) + soff[i];
+      else src = (k0 < p.K1) ? asrc[i] + k0 + soff[i] : a2src[i] + (k0 - p.K1) + soff[i];
       glds16(src, (PDM_LDS void*)(slot + piece * 1024));
       glds16(wsrc[i] + k0 + soff[i], (PDM_LDS void*)(slot + BM2 * ROWB + piece * 1024));
     }
@@ -243,87 +448,183 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs p, int tiles_n
     }
   }
 
-  if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
-    // bf16 epilogue staged through LDS (the ring is free now): the 256x256 bf16 tile (128 KiB) is written
-    // with a row-XOR chunk swizzle, then stored row-contiguously with 16-byte stores (full lines, half the
-    // store instructions of the per-lane 8-byte scatter).
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  f32x4 flat[32];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int nl = wn * 64 + ni * 16 + (lane >> 4) * 4;       // column within the tile
-      const int n = n0 + nl;
-      f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (p.bias && n < p.N) b = *reinterpret_cast<const f32x4*>(p.bias + n);
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
-        const int ml = wm * 128 + mi * 16 + (lane & 15);
-        f32x4 v = acc[ni][mi] + b;
-        if constexpr (EPI == EPI_GELU) {
-          v[0] = gelu_erf(v[0]); v[1] = gelu_erf(v[1]); v[2] = gelu_erf(v[2]); v[3] = gelu_erf(v[3]);
-        }
-        const int off = ml * 512 + ((((nl >> 3) ^ (ml & 31)) << 4) | ((nl & 4) << 1));
-        *reinterpret_cast<bf16x4*>(smem + off) = to_bf16x4(v[0], v[1], v[2], v[3]);
-      }
-    }
-    __syncthreads();
-#pragma unroll 4
-    for (int it = 0; it < 16; ++it) {
-      const int idx = it * 512 + tid;
-      const int ml = idx >> 5, ch = idx & 31;
-      const int m = m0 + ml, n = n0 + ch * 8;
-      const i32x4 v = *reinterpret_cast<const i32x4*>(smem + ml * 512 + ((ch ^ (ml & 31)) << 4));
-      if (m < p.M && n < p.N) *reinterpret_cast<i32x4*>(p.out_bf16 + (size_t)m * p.ldo + n) = v;
-    }
-    return;
+  for (int f = 0; f < 32; ++f) flat[f] = acc[f / 8][f % 8];
+  epilogue256<EPI, 0>(p, flat, smem, m0, n0, tid, lane, wm, wn);
+}
+
+// ------------------------------------------------------------------------------------------------
+// 256x256x64 tile, 8 waves, 8-phase schedule (2 LDS buffers x 4 half-tiles).  Each K-tile is staged as four
+// 16 KiB half-tiles (A rows 0-127 / 128-255, W rows 0-127 / 128-255), one per phase, two K-tiles' worth of
+// buffers; the block's 256x256 output is cut into quadrants (qi = A half, qj = W half) and every wave owns a
+// 64x32 piece of each quadrant, so phase q needs only the two half-tiles of its quadrant.  Phase order
+// (0,0) (0,1) (1,1) (1,0) reads 12 / 4 / 8 / 0 fragments (W fragments of both halves stay in registers).
+// Each phase: fragment reads, one half-tile LDS-DMA of the next K-tile, counted vmcnt (2 half-tiles stay
+// in flight), barrier, 16 MFMAs at raised priority, barrier.  Waves 4-7 run one barrier behind waves 0-3
+// (one extra barrier up front), so on every SIMD one wave computes while its partner reads/stages.
+// Requires K % 128 == 0 (an even number of K-tiles).
+__device__ __forceinline__ void bar_raw() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int EPI, int CONV>
+__global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs p, int tiles_n, int nwg) {
+  constexpr int ROWB = 128;                     // 64 bf16 per LDS row
+  constexpr int HALF = 128 * ROWB;              // 16 KiB half-tile
+  constexpr int BUF = 4 * HALF;                 // A0 A1 W0 W1
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
   }
-  // fp32 residual epilogue staged through LDS in two 128-row passes (128 KiB each): the accumulator tile
-  // is written with a row-XOR chunk swizzle, then every thread owns 8 consecutive columns of a row:
-  // 2 x 16-byte residual loads, 2 x 16-byte stores and one 16-byte bf16 copy store per row chunk.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    if (wm == pass) {
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const int nl = wn * 64 + ni * 16 + (lane >> 4) * 4;
-        const int n = n0 + nl;
-        f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (p.bias && n < p.N) b = *reinterpret_cast<const f32x4*>(p.bias + n);
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-          const int ml = mi * 16 + (lane & 15);
-          *reinterpret_cast<f32x4*>(smem + ml * 1024 + (((nl >> 2) ^ (ml & 63)) << 4)) = acc[ni][mi] + b;
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll 2
-    for (int it = 0; it < 8; ++it) {
-      const int idx = it * 512 + tid;
-      const int ml = idx >> 5, c8 = idx & 31;
-      const int m = m0 + pass * 128 + ml, n = n0 + c8 * 8;
-      f32x4 v0 = *reinterpret_cast<const f32x4*>(smem + ml * 1024 + (((2 * c8) ^ (ml & 63)) << 4));
-      f32x4 v1 = *reinterpret_cast<const f32x4*>(smem + ml * 1024 + (((2 * c8 + 1) ^ (ml & 63)) << 4));
-      if (m < p.M && n < p.N) {
-        f32x4* r = reinterpret_cast<f32x4*>(p.out_f32 + (size_t)m * p.ldr + n);
-        if (p.accumulate) {
-          v0 += r[0];
-          v1 += r[1];
-        }
-        r[0] = v0;
-        r[1] = v1;
-        if (p.out_bf16) {
-          bf16x8 o;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { o[j] = (bf16)v0[j]; o[4 + j] = (bf16)v1[j]; }
-          *reinterpret_cast<bf16x8*>(p.out_bf16 + (size_t)m * p.ldo + n) = o;
-        }
-      }
-    }
-    __syncthreads();
+  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  if (p.batch > 1) {
+    const long long z = blockIdx.y;
+    p.A1 += z * p.sA;
+    p.W += z * p.sW;
+    if (p.out_bf16) p.out_bf16 += z * p.sO;
+    if (p.out_f32) p.out_f32 += z * p.sR;
   }
+  const int ldw = p.ldw > 0 ? p.ldw : p.K;
+
+  // this lane's LDS-DMA sources: half h, piece i (8 rows x 128 B per wave-instruction), lane -> (row, chunk)
+  const int prow = lane >> 3, pch = lane & 7;
+  const bf16* a1src[2][2];
+  const bf16* a2src[2][2];
+  const bf16* wsrc[2][2];
+  int soff[2];
+  int cpix[2][2], cb[2][2];   // conv: packed (y << 16 | x) and image of the piece row
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + prow;           // row within the half-tile (0..127)
+    soff[i] = (pch ^ ((row >> 1) & 7)) * 8;               // logical chunk stored at physical pch
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int gm = m0 + h * 128 + row;
+      gm = gm < p.M ? gm : p.M - 1;
+      const int gm1 = (!CONV && p.a_rows_per_group > 0) ? (gm / p.a_rows_per_group) * p.a_group_stride + gm % p.a_rows_per_group : gm;
+      a1src[h][i] = p.A1 + (size_t)gm1 * p.lda1;
+      a2src[h][i] = p.A2 ? p.A2 + (size_t)gm * p.lda2 : p.A1;
+      if constexpr (CONV) {
+        const int hw = p.convH * p.convW;
+        cb[h][i] = gm / hw;
+        const int r = gm - cb[h][i] * hw;
+        const int y = r / p.convW;
+        cpix[h][i] = (y << 16) | (r - y * p.convW);
+      }
+      int gn = n0 + h * 128 + row;
+      gn = gn < p.N ? gn : p.N - 1;
+      wsrc[h][i] = p.W + (size_t)gn * ldw;
+    }
+  }
+
+  // half-tile kinds: 0 = A rows 0-127, 1 = A rows 128-255, 2 = W rows 0-127, 3 = W rows 128-255
+  auto issue = [&](int kt, int kind) {
+    const int k0 = kt * 64;
+    char* dst = smem + (kt & 1) * BUF + kind * HALF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int piece = wave * 2 + i;
+      const bf16* src;
+      if (kind >= 2) {
+        src = wsrc[kind - 2][i] + k0 + soff[i];
+      } else if constexpr (CONV) {
+        const int pix = cpix[kind][i];
+        src = conv_row_ptr(p, p.A1, cb[kind][i], pix >> 16, pix & 0xffff, k0) + soff[i];
+      } else {
+        src = (k0 < p.K1) ? a1src[kind][i] + k0 + soff[i] : a2src[kind][i] + (k0 - p.K1) + soff[i];
+      }
+      glds16(src, (PDM_LDS void*)(dst + piece * 1024));
+    }
+  };
+
+  f32x4 acc[32];
+#pragma unroll
+  for (int f = 0; f < 32; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2];      // A fragments of the current A half: [mi][k-sub]
+  bf16x8 wf[2][2][2];   // W fragments of both W halves: [qj][ni][k-sub]
+
+  auto read_a = [&](const char* buf, int qi) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int row = qi * 128 + wm * 64 + mi * 16 + (lane & 15);   // row within the 256-row A image
+        af[mi][ks] = *reinterpret_cast<const bf16x8*>(buf + (row >> 7) * HALF + swz_off<64>(row & 127, ks * 4 + (lane >> 4)));
+      }
+  };
+  auto read_w = [&](const char* buf, int qj) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int row = wn * 32 + ni * 16 + (lane & 15);
+        wf[qj][ni][ks] = *reinterpret_cast<const bf16x8*>(buf + (2 + qj) * HALF + swz_off<64>(row, ks * 4 + (lane >> 4)));
+      }
+  };
+  auto mma = [&](int qi, int qj) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          f32x4& c = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
+          c = mfma16x16x32(wf[qj][ni][ks], af[mi][ks], c);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = p.K / 64;
+  issue(0, 0);
+  issue(0, 2);
+  issue(0, 3);
+  issue(0, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // A0, W0 of K-tile 0 landed (this wave's share)
+  bar_raw();
+  if (wave >= 4) bar_raw();                            // stagger: waves 4-7 one barrier behind
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* buf = smem + (kt & 1) * BUF;
+    const bool more = kt + 1 < nk;
+    // phase 1: quadrant (0,0)
+    read_a(buf, 0);
+    read_w(buf, 0);
+    if (more) { issue(kt + 1, 0); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }   // W1(kt) landed
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    bar_raw();
+    mma(0, 0);
+    bar_raw();
+    // phase 2: quadrant (0,1)
+    read_w(buf, 1);
+    if (more) { issue(kt + 1, 2); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }   // A1(kt) landed
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar_raw();
+    mma(0, 1);
+    bar_raw();
+    // phase 3: quadrant (1,1)
+    read_a(buf, 1);
+    if (more) issue(kt + 1, 3);
+    bar_raw();
+    mma(1, 1);
+    bar_raw();
+    // phase 4: quadrant (1,0) on fragments already in registers
+    if (more) { issue(kt + 1, 1); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }   // A0, W0(kt+1) landed
+    bar_raw();
+    mma(1, 0);
+    bar_raw();
+  }
+  if (wave < 4) bar_raw();                             // rejoin the stagger
+
+  epilogue256<EPI, 1>(p, acc, smem, m0, n0, tid, lane, wm, wn);
 }
 }  // namespace
 
@@ -335,6 +636,13 @@ const char* gemm_check(const GemmArgs& p, int epi) {
   if (p.K1 < p.K && !p.A2) return "gemm: split-K operand A2 missing";
   if (!p.A1 || !p.W) return "gemm: null operand";
   if ((p.lda1 % 8) || (p.K1 < p.K && (p.lda2 % 8))) return "gemm: lda must be a multiple of 8 (16-byte rows)";
+  if (p.ldw && (p.ldw < p.K || p.ldw % 8)) return "gemm: ldw must be >= K and a multiple of 8";
+  if (p.conv) {
+    if (p.convC % BK || p.K != 9 * p.convC) return "gemm(conv): C_in must be a multiple of 64 and K = 9 * C_in";
+    if (!p.zero || ((uintptr_t)p.zero & 15)) return "gemm(conv): zero page missing";
+    if (p.A2 || p.a_rows_per_group) return "gemm(conv): no split-K / row gather in conv mode";
+    if (p.conv_up && (p.convH % 2 || p.convW % 2)) return "gemm(conv): upsampled grid must be even";
+  }
   if (((uintptr_t)p.A1 | (uintptr_t)p.W | (uintptr_t)(p.A2 ? p.A2 : p.A1)) & 15) return "gemm: operands must be 16-byte aligned";
   if (epi == EPI_BF16 || epi == EPI_GELU) {
     if (!p.out_bf16 || (p.ldo % 4)) return "gemm: bf16 output missing or ldo not a multiple of 4";
@@ -347,7 +655,7 @@ const char* gemm_check(const GemmArgs& p, int epi) {
   return nullptr;
 }
 
-static int g_gemm_algo = 0;  // 0 auto, 1 = 128x128, 2 = 256x256 BK32 x4 ring, 3 = 256x256 BK64 x2
+static int g_gemm_algo = 0;  // 0 auto, 1 = 128x128, 2 = 256x256 BK32 x4 ring, 3 = 256x256 BK64 x2, 4 = 256x256 8-phase
 void gemm_set_algo(int algo) { g_gemm_algo = algo; }
 
 template <int BK, int NS>
@@ -362,11 +670,32 @@ static hipError_t launch256(const GemmArgs& p, int epi, hipStream_t stream) {
   }
   const int tn = (p.N + BN2 - 1) / BN2, tm = (p.M + BM2 - 1) / BM2;
   const int nwg = tm * tn;
-  dim3 grid(nwg), block(512);
+  dim3 grid(nwg, p.batch > 1 ? p.batch : 1), block(512);
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL((gemm256_kernel<EPI_BF16, BK, NS>), grid, block, SMEM, stream, p, tn, nwg); break;
     case EPI_GELU: hipLaunchKernelGGL((gemm256_kernel<EPI_GELU, BK, NS>), grid, block, SMEM, stream, p, tn, nwg); break;
     default: hipLaunchKernelGGL((gemm256_kernel<EPI_F32, BK, NS>), grid, block, SMEM, stream, p, tn, nwg); break;
+  }
+  return hipGetLastError();
+}
+
+template <int CONV>
+static hipError_t launch8p(const GemmArgs& p, int epi, hipStream_t stream) {
+  constexpr int SMEM = 2 * 4 * 128 * 128;   // 128 KiB
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI_BF16, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI_GELU, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI_F32, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr_set = true;
+  }
+  const int tn = (p.N + BN2 - 1) / BN2, tm = (p.M + BM2 - 1) / BM2;
+  const int nwg = tm * tn;
+  dim3 grid(nwg, p.batch > 1 ? p.batch : 1), block(512);
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL((gemm8p_kernel<EPI_BF16, CONV>), grid, block, SMEM, stream, p, tn, nwg); break;
+    case EPI_GELU: hipLaunchKernelGGL((gemm8p_kernel<EPI_GELU, CONV>), grid, block, SMEM, stream, p, tn, nwg); break;
+    default: hipLaunchKernelGGL((gemm8p_kernel<EPI_F32, CONV>), grid, block, SMEM, stream, p, tn, nwg); break;
   }
   return hipGetLastError();
 }
@@ -379,11 +708,12 @@ hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream) {
   if (epi == EPI_F32 && (p.N % 8 || p.ldr % 4 || ((uintptr_t)p.out_f32 & 15) ||
                          (p.out_bf16 && (p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))))) algo = 1;
   if (algo == 2 && p.K % 32 == 0) return launch256<32, 4>(p, epi, stream);
-  if (algo == 3 && p.K % 64 == 0) return launch256<64, 2>(p, epi, stream);
+  if (algo == 4 && p.K % 128 == 0) return p.conv ? launch8p<1>(p, epi, stream) : launch8p<0>(p, epi, stream);
+  if ((algo == 3 || algo == 4) && p.K % 64 == 0) return launch256<64, 2>(p, epi, stream);
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles_m = (p.M + BM - 1) / BM;
   const int nwg = tiles_m * tiles_n;
-  dim3 grid(nwg), block(256);
+  dim3 grid(nwg, p.batch > 1 ? p.batch : 1), block(256);
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_BF16>, grid, block, SMEM_BYTES, stream, p, tiles_n, nwg); break;
     case EPI_GELU: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_GELU>, grid, block, SMEM_BYTES, stream, p, tiles_n, nwg); break;

@@ -1,6 +1,8 @@
 // Internal launcher declarations shared by the kernels and the C-ABI layer.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <string>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -22,6 +24,13 @@ struct GemmArgs {
   int accumulate;             // EPI_F32: out_f32 += result (residual add) instead of =
   int a_rows_per_group;       // >0: A1 row m is read from (m / rpg) * a_group_stride + m % rpg
   int a_group_stride;
+  int ldw;                    // W row stride (0 -> K)
+  int batch;                  // >1: blockIdx.y selects A1 + z*sA, W + z*sW, out_bf16 + z*sO, out_f32 + z*sR
+  long long sA, sW, sO, sR;
+  // implicit-GEMM conv3x3 (stride 1, pad 1) over an NHWC bf16 A1 [B, Hs, Ws, convC]: row m = output pixel
+  // (b, y, x) of an convH x convW grid, K = 9 * convC in (ky, kx, ci) order, padded taps read `zero`.
+  int conv, convH, convW, convC, conv_up;   // conv_up: source is the nearest-x2 upsample (Hs = H/2)
+  const bf16* zero;           // >= 256 zero bytes
 };
 
 const char* gemm_check(const GemmArgs& p, int epi);
@@ -111,6 +120,9 @@ struct EpilogueArgs {
 };
 const char* epilogue_check(const EpilogueArgs& p);
 hipError_t epilogue_launch(const EpilogueArgs& p, hipStream_t stream);
+
+// records `msg` as pdm_last_error() (capi.hip) and returns `code`
+int set_error(int code, const std::string& msg);
 
 hipError_t cast_bf16_launch(const float* x, bf16* y, long long n, hipStream_t stream);
 

@@ -5,12 +5,17 @@ reference's state_dict keys for `post_quant_conv.*` and `decoder.*` (the encoder
 checkpoint are accepted and ignored), so `get_model(path)` loads the reference's
 assets/stable-diffusion/autoencoder_kl*.pth with `torch.load(..., weights_only=True)`.
 
-INTERIM (round 1): the decoder's convolutions / GroupNorm run as PyTorch-ROCm (MIOpen) ops in bf16 on the
-GPU.  The hand-written implicit-GEMM HIP decoder is the next row of SURVEY.md §8(f).
+`decode` runs the hand-written HIP decoder of libpdm (csrc/decoder.hip, `pdm_decoder_*` in include/pdm.h):
+NHWC activations, fp32 residual stream, every 3x3 conv an implicit GEMM on the bf16 MFMA GEMM kernels with
+GroupNorm+swish fused into the producer of its bf16 input.  On first use the fp32 parameters are repacked
+once (3x3 convs -> bf16 [Cout][ky][kx][Cin]; q/k/v -> one [3C, C] matrix; conv_out padded to 4 rows).
+Large batches are decoded in chunks of `chunk` latents (the reference decodes in chunks of 50,
+decode_large_batch in eval_ldm_discrete.py:62-68) so the workspace stays bounded.
 """
+import ctypes
+
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .. import _lib
 from .. import weights as W
@@ -18,22 +23,97 @@ from .. import weights as W
 DDCONFIG = dict(W.DECODER_DDCONFIG)
 
 
-def _gn_swish(x, w, b):
-    return F.silu(F.group_norm(x, 32, w, b, eps=1e-6))
+class _DecoderHandle:
+    """pdm_decoder handle + packed device copies of the weights it points at."""
+
+    def __init__(self, module, device):
+        lib = _lib.load()
+        cfg = _lib.PdmDecoderCfg()
+        cfg.ch = module.ch
+        for i, m in enumerate(module.ch_mult):
+            cfg.ch_mult[i] = m
+        cfg.num_levels = len(module.ch_mult)
+        cfg.num_res_blocks = module.num_res_blocks
+        cfg.z_channels = module.z_channels
+        cfg.out_ch = module.out_ch
+        cfg.latent_size = module.latent_size
+        cfg.scale_factor = module.scale_factor
+        h = ctypes.c_void_p()
+        _lib.check(lib.pdm_decoder_create(ctypes.byref(cfg), ctypes.byref(h)), "pdm_decoder_create")
+        self.lib, self.h, self.device = lib, h, device
+        self.packed = {}
+        self.ws = None
+        self.ws_batch = 0
+        buf = ctypes.create_string_buffer(256)
+        for i in range(lib.pdm_decoder_param_count(h)):
+            dt, numel = ctypes.c_int(), ctypes.c_longlong()
+            _lib.check(lib.pdm_decoder_param_info(h, i, buf, 256, ctypes.byref(dt), ctypes.byref(numel)))
+            name = buf.value.decode()
+            t = self._pack(module, name, dt.value).to(device).contiguous()
+            if t.numel() != numel.value:
+                raise RuntimeError(f"decoder weight {name}: packed {t.numel()} elements, expected {numel.value}")
+            self.packed[name] = t
+            _lib.check(lib.pdm_decoder_set_param(h, name.encode(), _lib.ptr(t), dt.value, t.numel()),
+                       "pdm_decoder_set_param")
+
+    @staticmethod
+    def _pack(m, name, dtype):
+        if name.endswith("mid.attn_1.qkv.weight"):
+            p = name[: -len("qkv.weight")]
+            w = torch.cat([m._p(p + f"{n}.weight") for n in "qkv"]).reshape(-1, m._p(p + "q.weight").shape[1])
+            return w.to(torch.bfloat16)
+        if name.endswith("mid.attn_1.qkv.bias"):
+            p = name[: -len("qkv.bias")]
+            return torch.cat([m._p(p + f"{n}.bias") for n in "qkv"]).float()
+        src = m._p(name).detach().float()
+        if name == "decoder.conv_out.weight":   # [out_ch, C, 3, 3] -> [4][ky][kx][C], zero rows
+            w = torch.zeros(4, *src.shape[1:], dtype=src.dtype, device=src.device)
+            w[: src.shape[0]] = src
+            return w.permute(0, 2, 3, 1).reshape(4, -1).to(torch.bfloat16)
+        if name == "decoder.conv_out.bias":
+            b = torch.zeros(4, dtype=src.dtype, device=src.device)
+            b[: src.shape[0]] = src
+            return b
+        if dtype == _lib.PDM_BF16:
+            if src.dim() == 4 and src.shape[-1] == 3:   # 3x3 conv -> [Cout][ky][kx][Cin]
+                return src.permute(0, 2, 3, 1).reshape(src.shape[0], -1).to(torch.bfloat16)
+            return src.reshape(src.shape[0], -1).to(torch.bfloat16)   # 1x1 conv
+        return src.reshape(-1)
+
+    def workspace(self, batch):
+        if self.ws is None or self.ws_batch < batch:
+            nbytes = ctypes.c_size_t()
+            _lib.check(self.lib.pdm_decoder_workspace_size(self.h, batch, ctypes.byref(nbytes)),
+                       "pdm_decoder_workspace_size")
+            self.ws = None
+            self.ws = torch.empty(nbytes.value, dtype=torch.uint8, device=self.device)
+            self.ws_batch = batch
+        return self.ws
+
+    def __del__(self):
+        try:
+            self.lib.pdm_decoder_destroy(self.h)
+        except Exception:
+            pass
 
 
 class FrozenAutoencoderKL(nn.Module):
     def __init__(self, ddconfig=None, embed_dim=4, pretrained_path=None, scale_factor=0.18215, seed=0,
-                 dtype=torch.bfloat16, state_dict=None):
+                 dtype=torch.bfloat16, state_dict=None, latent_size=32, chunk=32):
         super().__init__()
         dd = dict(DDCONFIG if ddconfig is None else ddconfig)
+        self.ch = int(dd["ch"])
         self.ch_mult = tuple(dd["ch_mult"])
-        self.num_res_blocks = dd["num_res_blocks"]
-        self.scale_factor = scale_factor
+        self.num_res_blocks = int(dd["num_res_blocks"])
+        self.z_channels = int(dd["z_channels"])
+        self.out_ch = int(dd["out_ch"])
+        self.scale_factor = float(scale_factor)
         self.embed_dim = embed_dim
         self.compute_dtype = dtype
-        spec = W.decoder_spec(ch=dd["ch"], out_ch=dd["out_ch"], ch_mult=self.ch_mult,
-                              num_res_blocks=self.num_res_blocks, z_channels=dd["z_channels"], embed_dim=embed_dim)
+        self.latent_size = int(latent_size)
+        self.chunk = int(chunk)
+        spec = W.decoder_spec(ch=self.ch, out_ch=self.out_ch, ch_mult=self.ch_mult,
+                              num_res_blocks=self.num_res_blocks, z_channels=self.z_channels, embed_dim=embed_dim)
         if state_dict is not None or pretrained_path is not None:
             full = state_dict if state_dict is not None else torch.load(pretrained_path, map_location="cpu",
                                                                         weights_only=True)
@@ -48,50 +128,46 @@ class FrozenAutoencoderKL(nn.Module):
             self.register_buffer(k.replace(".", "__"), sd[k].float().clone())
         self.requires_grad_(False)
         self.eval()
+        self._native = None
 
     def _p(self, name):
         return getattr(self, name.replace(".", "__"))
 
-    def _conv(self, name, x, pad):
-        return F.conv2d(x, self._p(f"{name}.weight").to(x.dtype), self._p(f"{name}.bias").to(x.dtype), padding=pad)
+    def _apply(self, fn, *a, **kw):
+        self._native = None
+        return super()._apply(fn, *a, **kw)
 
-    def _res(self, p, x):
-        h = self._conv(f"{p}.conv1", _gn_swish(x, self._p(f"{p}.norm1.weight").to(x.dtype), self._p(f"{p}.norm1.bias").to(x.dtype)), 1)
-        h = self._conv(f"{p}.conv2", _gn_swish(h, self._p(f"{p}.norm2.weight").to(x.dtype), self._p(f"{p}.norm2.bias").to(x.dtype)), 1)
-        if hasattr(self, f"{p}.nin_shortcut.weight".replace(".", "__")):
-            x = self._conv(f"{p}.nin_shortcut", x, 0)
-        return x + h
+    def _load_from_state_dict(self, *a, **kw):
+        self._native = None
+        return super()._load_from_state_dict(*a, **kw)
 
-    def _attn(self, p, x):
-        h = F.group_norm(x, 32, self._p(f"{p}.norm.weight").to(x.dtype), self._p(f"{p}.norm.bias").to(x.dtype), eps=1e-6)
-        q = self._conv(f"{p}.q", h, 0)
-        k = self._conv(f"{p}.k", h, 0)
-        v = self._conv(f"{p}.v", h, 0)
-        b, c, hh, ww = q.shape
-        q = q.reshape(b, c, hh * ww).transpose(1, 2)[:, None]
-        k = k.reshape(b, c, hh * ww).transpose(1, 2)[:, None]
-        v = v.reshape(b, c, hh * ww).transpose(1, 2)[:, None]
-        o = F.scaled_dot_product_attention(q, k, v)[:, 0].transpose(1, 2).reshape(b, c, hh, ww)
-        return x + self._conv(f"{p}.proj_out", o, 0)
+    def native(self, device):
+        if self._native is None or self._native.device != device:
+            self._native = _DecoderHandle(self, device)
+        return self._native
 
     @torch.no_grad()
     def decode(self, z):
-        """libs/autoencoder.py:446-450 + Decoder.forward 376-409."""
+        """libs/autoencoder.py:446-450 (z / scale_factor -> post_quant_conv -> Decoder.forward 376-409)."""
         _lib.require_gpu(z)
-        x = (z.float() / self.scale_factor).to(self.compute_dtype).contiguous(memory_format=torch.channels_last)
-        x = self._conv("post_quant_conv", x, 0)
-        h = self._conv("decoder.conv_in", x, 1)
-        h = self._res("decoder.mid.block_1", h)
-        h = self._attn("decoder.mid.attn_1", h)
-        h = self._res("decoder.mid.block_2", h)
-        for i_level in reversed(range(len(self.ch_mult))):
-            for i_block in range(self.num_res_blocks + 1):
-                h = self._res(f"decoder.up.{i_level}.block.{i_block}", h)
-            if i_level != 0:
-                h = F.interpolate(h, scale_factor=2.0, mode="nearest")
-                h = self._conv(f"decoder.up.{i_level}.upsample.conv", h, 1)
-        h = _gn_swish(h, self._p("decoder.norm_out.weight").to(h.dtype), self._p("decoder.norm_out.bias").to(h.dtype))
-        return self._conv("decoder.conv_out", h, 1).float()
+        B, C, h, w = z.shape
+        if C != self.z_channels or h != self.latent_size or w != self.latent_size:
+            if h == w and C == self.z_channels:   # another latent size: a handle per size
+                self.latent_size = h
+                self._native = None
+            else:
+                raise ValueError(f"decode: expected z [B, {self.z_channels}, s, s], got {tuple(z.shape)}")
+        nat = self.native(z.device)
+        z = z.float().contiguous()
+        up = 2 ** (len(self.ch_mult) - 1)
+        img = torch.empty(B, self.out_ch, h * up, w * up, dtype=torch.float32, device=z.device)
+        stream = _lib.stream_ptr(z.device)
+        for s in range(0, B, self.chunk):
+            n = min(self.chunk, B - s)
+            ws = nat.workspace(min(self.chunk, B))
+            _lib.check(nat.lib.pdm_decoder_decode(nat.h, _lib.ptr(z[s:s + n]), _lib.ptr(img[s:s + n]), n,
+                                                  _lib.ptr(ws), ws.numel(), stream), "pdm_decoder_decode")
+        return img
 
     def forward(self, inputs, fn):
         if fn == "decode":

@@ -102,8 +102,9 @@ class ClassCondSampler:
                 k += 1
 
     @torch.no_grad()
-    def sample(self, z, y=None):
-        """z [B, C, H, W] fp32 on the GPU; y [B] int64 labels (num_classes > 0).  Returns z_0 [B, C, H, W]."""
+    def sample(self, z, y=None, eager=False):
+        """z [B, C, H, W] fp32 on the GPU; y [B] int64 labels (num_classes > 0).  Returns z_0 [B, C, H, W].
+        eager=True runs this call without the HIP graph (e.g. with the GEMM profiling hook enabled)."""
         _lib.require_gpu(z)
         B = z.shape[0]
         st = self._buffers(B, z.device)
@@ -117,7 +118,7 @@ class ClassCondSampler:
             st["y"][:B].copy_(y)
             if self.cfg:
                 st["y"][B:].fill_(self.null_label)
-        if not self.use_graph:
+        if not self.use_graph or eager:
             self._loop(st, B)
             return st["x"].clone()
         if st["graph"] is None:

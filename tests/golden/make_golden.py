@@ -353,6 +353,32 @@ def gen_decoder(mods, out):
     out["decoder/img"] = _np(img)
 
 
+def gen_decoder64(mods, out):
+    """64/128-channel decoder (the HIP decoder needs channel counts that are multiples of 64) and the
+    full KL-f8 decoder (ddconfig of libs/autoencoder.py:471-484) on one 32x32 latent, seeded weights."""
+    ae = mods[2]
+    cases = [("decoder64", dict(ch=64, ch_mult=[1, 2], num_res_blocks=1), 7, (2, 4, 8, 8), "random"),
+             ("decoder_full", dict(ch=128, ch_mult=[1, 2, 4, 4], num_res_blocks=2), 1, (1, 4, 32, 32), "reference")]
+    for key, kw, seed, zshape, init in cases:
+        ddc = dict(double_z=True, z_channels=4, resolution=256, in_channels=3, out_ch=3, attn_resolutions=[],
+                   dropout=0.0, **kw)
+        dec = ae.Decoder(**ddc)
+        sd = W.make_state_dict(W.decoder_spec(ch=kw["ch"], ch_mult=tuple(kw["ch_mult"]),
+                                              num_res_blocks=kw["num_res_blocks"], prefix="decoder"),
+                               seed=seed, init=init)
+        dec.load_state_dict({k[len("decoder."):]: v for k, v in sd.items() if k.startswith("decoder.")})
+        dec.eval()
+        pq = torch.nn.Conv2d(4, 4, 1)
+        pq.load_state_dict({"weight": sd["post_quant_conv.weight"], "bias": sd["post_quant_conv.bias"]})
+        g = torch.Generator().manual_seed(seed + 100)
+        z = torch.randn(*zshape, generator=g)
+        with torch.no_grad():
+            img = dec(pq(z / 0.18215))
+        out[f"{key}/sd_checksum"] = _sd_checksum(sd)
+        out[f"{key}/z"] = _np(z)
+        out[f"{key}/img"] = _np(img)
+
+
 def gen_utils(ref, out):
     f = _ref_funcs(os.path.join(ref, "utils.py"), ["int2bits", "bits2int", "amortize"])
     g = torch.Generator().manual_seed(23)
@@ -376,6 +402,7 @@ def main():
     gen_solver(mods, out)
     gen_sample_tiny(mods, out)
     gen_decoder(mods, out)
+    gen_decoder64(mods, out)
     gen_utils(ref, out)
     path = os.path.join(HERE, "golden.npz")
     np.savez_compressed(path, **{k: np.asarray(v) for k, v in out.items()})

@@ -59,6 +59,35 @@ def test_gemm_split_k(lib):
     assert rel(out, ref) < 2e-3
 
 
+@pytest.mark.parametrize("algo", [1, 2, 3, 4])
+@pytest.mark.parametrize("M,N,K", [(4133, 1000, 1024), (515, 768, 2048), (8192, 512, 128)])
+@pytest.mark.parametrize("epi", ["gelu", "f32acc_copy", "split"])
+def test_gemm_algos(lib, algo, M, N, K, epi):
+    """Every tile policy (1: 128x128, 2/3: 256x256 ring, 4: 256x256 8-phase staggered) on ragged M/N tails."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + algo)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    ref = a.float() @ w.float().t() + bias
+    lib.load().pdm_set_gemm_algo(algo)
+    try:
+        if epi == "gelu":
+            out = lib.gemm(a, w, bias, lib.EPI_GELU)
+            assert rel(out.float(), F.gelu(ref)) < 1e-2
+        elif epi == "f32acc_copy":
+            r0 = torch.randn(M, N, device="cuda", generator=g)
+            cp = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            out = lib.gemm(a, w, bias, lib.EPI_F32, out=cp, out_f32=r0.clone(), accumulate=True)
+            assert rel(out, ref + r0) < 2e-3
+            assert rel(cp.float(), ref + r0) < 1e-2
+        else:
+            h = K // 2
+            out = lib.gemm(a[:, :h].contiguous(), w, bias, lib.EPI_F32, a2=a[:, h:].contiguous())
+            assert rel(out, ref) < 2e-3
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+
+
 def test_gemm_bad_shape(lib):
     a = torch.zeros(16, 100, device="cuda", dtype=torch.bfloat16)
     w = torch.zeros(128, 100, device="cuda", dtype=torch.bfloat16)

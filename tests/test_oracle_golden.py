@@ -173,6 +173,18 @@ def test_decoder(golden):
     assert rel_l2(img, golden["decoder/img"]) < 1e-5
 
 
+@pytest.mark.parametrize("key,ch,mult,nrb,seed,init", [
+    ("decoder64", 64, (1, 2), 1, 7, "random"),
+    ("decoder_full", 128, (1, 2, 4, 4), 2, 1, "reference"),
+])
+def test_decoder_sizes(golden, key, ch, mult, nrb, seed, init):
+    sd = W.make_state_dict(W.decoder_spec(ch=ch, ch_mult=mult, num_res_blocks=nrb), seed=seed, init=init)
+    chk = np.array([float(v.double().sum()) for v in sd.values()] + [float(v.double().abs().sum()) for v in sd.values()])
+    np.testing.assert_allclose(chk, golden[f"{key}/sd_checksum"], rtol=1e-12, atol=1e-9)
+    img = autoencoder_ref.decode(sd, torch.from_numpy(golden[f"{key}/z"]), ch_mult=mult, num_res_blocks=nrb)
+    assert rel_l2(img, golden[f"{key}/img"]) < 1e-5
+
+
 def test_utils(golden):
     ids = golden["utils/ids"]
     np.testing.assert_array_equal(utils_ref.int2bits(ids), golden["utils/bits"].astype(np.int64))

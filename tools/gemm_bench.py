@@ -44,14 +44,29 @@ for name, N, K, epi in shapes:
             e1.record()
             torch.cuda.synchronize()
             times[algo].append(e0.elapsed_time(e1) / 10)
+    # vendor reference point: hipBLASLt via torch (bf16 out, bias, no fused epilogue)
+    bl = []
+    for rnd in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        bb = bias.bfloat16()
+        e0.record()
+        for _ in range(10):
+            torch.nn.functional.linear(a, W, bb)
+        e1.record()
+        torch.cuda.synchronize()
+        bl.append(e0.elapsed_time(e1) / 10)
     f = 2.0 * M * N * K
     flops += f
+    tbl = sorted(bl)[2]
+    tot["blas"] = tot.get("blas", 0.0) + tbl
     line = f"{name:5s} M={M} N={N} K={K} maxrelerr={err:.1e}"
     for algo in ALGOS:
         t = sorted(times[algo])[len(times[algo]) // 2]
         tot[algo] += t
         line += f" | algo{algo} {t*1e3:8.1f} us {f/t/1e9:7.1f} TF/s"
+    line += f" | hipblaslt {tbl*1e3:8.1f} us {f/tbl/1e9:7.1f} TF/s"
     print(line)
+print(f"hipblaslt: block GEMMs {tot['blas']:.3f} ms -> {flops/tot['blas']/1e9:.1f} TF/s")
 for algo in ALGOS:
     print(f"algo{algo}: block GEMMs {tot[algo]:.3f} ms -> {flops/tot[algo]/1e9:.1f} TF/s")
 lib.pdm_set_gemm_algo(0)

@@ -1,0 +1,68 @@
+"""Turn a tools/profile_bench.sh run (gpurun_out/prof_TAG) into the committed evidence under profiles/:
+
+  profiles/TAG_bench_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the bench command
+  profiles/TAG_traffic.json             per-kernel HBM traffic per launch from the FETCH_SIZE / WRITE_SIZE
+                                        passes (FETCH_SIZE doubled: MI355X_MICROARCH.md §HBM, 16-B streaming
+                                        reads are tallied at half their bytes; values are KiB in rocprofv3)
+
+Usage: python tools/summarize_prof.py TAG
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    n = name.split("(")[0].replace("void ", "")
+    return n.replace("pdm::(anonymous namespace)::", "")
+
+
+def per_kernel(path, counter):
+    acc = defaultdict(lambda: [0.0, 0])
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        k = short(r["Kernel_Name"])
+        acc[k][0] += float(r["Counter_Value"])
+        acc[k][1] += 1
+    return {k: (v[0] / v[1], v[1]) for k, v in acc.items()}
+
+
+def main():
+    tag = sys.argv[1]
+    src = os.path.join(REPO, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(REPO, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    kt = os.path.join(src, "kt", "run_kernel_stats.csv")
+    if os.path.exists(kt):
+        shutil.copy(kt, os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))
+    fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over tools/time_forward.py "
+                     f"imagenet256_uvit_large 190 (one CFG forward at the bench batch, 95 images x 2 rows)",
+           "correction": "fetch_bytes = FETCH_SIZE[KiB] x 1024 x 2 (gfx950 tallies 16-B streaming reads at half); "
+                         "write_bytes = WRITE_SIZE[KiB] x 1024",
+           "kernels": {}}
+    gemm_f = gemm_w = gemm_n = 0.0
+    for k in sorted(set(fetch) | set(write)):
+        f, n = fetch.get(k, (0.0, 0))
+        w, _ = write.get(k, (0.0, 0))
+        fb, wb = f * 1024 * 2, w * 1024
+        out["kernels"][k] = {"launches": n, "fetch_bytes_per_launch": round(fb), "write_bytes_per_launch": round(wb)}
+        if k.startswith("gemm"):
+            gemm_f += fb * n
+            gemm_w += wb * n
+            gemm_n += n
+    if gemm_n:
+        out["gemm_family"] = {"launches": int(gemm_n), "hbm_bytes_per_launch": round((gemm_f + gemm_w) / gemm_n)}
+    json.dump(out, open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1)
+    print(json.dumps(out.get("gemm_family"), indent=1))
+
+
+if __name__ == "__main__":
+    main()

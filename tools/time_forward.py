@@ -10,6 +10,7 @@ from panopticdiffusionmodels_amd.utils import get_nnet  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "imagenet256_uvit_large"
 rows = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+n = int(sys.argv[3]) if len(sys.argv) > 3 else 10   # timed forwards
 dev = torch.device("cuda")
 cfg = configs.nnet_kwargs(name)
 sd = weights.nnet_state_dict(cfg, seed=0, device=dev)
@@ -23,7 +24,6 @@ with torch.no_grad():
     for _ in range(3):
         net.forward_pre(x, t, y)
     torch.cuda.synchronize()
-    n = 10
     t0 = time.perf_counter()
     for _ in range(n):
         net.forward_pre(x, t, y)
