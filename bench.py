@@ -97,7 +97,12 @@ def main():
     from panopticdiffusionmodels_amd import _lib
     prof = _lib.GemmProfiler(net.native(), max_launches=512)
 
-    def one_step(s, profile=False):
+    ev = []   # (start, after sampling, after decode) HIP events per timed step, on the launch stream
+
+    def one_step(s, profile=False, timed=False):
+        if timed:
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record()
         if profile:   # last timed step: eager launches with HIP events around every GEMM (libpdm hook)
             prof.enable()
             z = sampler.sample(zs[s], ys[s], eager=True)
@@ -105,11 +110,14 @@ def main():
         else:
             z = sampler.sample(zs[s], ys[s])
         if world > 1:
-            parallel.gather_latents(z)
-        if ae is not None:
-            img = ae.decode(z)
-            return img
-        return z
+            z = parallel.gather_latents(z)[rank * B:(rank + 1) * B]
+        if timed:
+            e[1].record()
+        out = ae.decode(z) if ae is not None else z
+        if timed:
+            e[2].record()
+            ev.append(e)
+        return out
 
     for s in range(args.warmup):
         one_step(s)
@@ -119,7 +127,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.warmup, nsteps):
-        out = one_step(s, profile=(s == nsteps - 1))
+        out = one_step(s, profile=(s == nsteps - 1), timed=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -134,6 +142,8 @@ def main():
     # ---- roofline of the dominant kernel (the bf16 GEMM family): HIP events recorded by libpdm on the launch
     # stream around every GEMM launch of the last forward of the last timed step
     roof = gemm_roofline(prof, ncfg, 2 * B if sampler.cfg else B)
+    samp_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
 
     images = world * B * args.steps
     value = images / elapsed
@@ -155,6 +165,9 @@ def main():
                    "model": "U-ViT-L/2", "per_gpu_batch": B, "global_batch": world * B,
                    "nfe": sampler.nfe, "hip_graph": not args.no_graph, "parallelism": f"dp{world} (batch-sharded)"},
         "roofline": roof,
+        "breakdown_ms_per_step": {"sample_50nfe": round(samp_ms, 2), "decode": round(dec_ms, 2),
+                                  "note": "HIP events on the launch stream; the last timed step samples eagerly "
+                                          "with per-GEMM events (graph replay in the others)"},
     }
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         res["cpu_baseline"] = cpu_baseline(full, ncfg, args.cpu_nfe, ae is not None)
@@ -164,15 +177,29 @@ def main():
         dist.destroy_process_group()
 
 
+def measured_traffic():
+    """HBM bytes per GEMM launch from the newest committed PMC summary (tools/profile_bench.sh +
+    tools/summarize_prof.py: FETCH_SIZE x 2 + WRITE_SIZE, separate rocprofv3 passes), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    fam = d.get("gemm_family")
+    return (fam["hbm_bytes_per_launch"] if fam else None), os.path.basename(files[-1])
+
+
 def gemm_roofline(prof, ncfg, rows):
     times_ms, flops = prof.read()
     n = len(times_ms)
     tot_t = sum(times_ms) / 1e3
     tot_f = sum(flops)
     achieved = tot_f / tot_t
-    return {"bound": "mfma", "kernel": "gemm256_kernel<*> (all U-ViT linear layers; qkv, proj, fc1, fc2, skip_linear)",
+    traffic, tsrc = measured_traffic()
+    return {"bound": "mfma", "kernel": "bf16 GEMM family (all U-ViT linear layers: qkv, proj, fc1, fc2, skip_linear)",
             "achieved": round(achieved / 1e12, 1), "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16, 4), "traffic": None,
+            "frac": round(achieved / PEAK_BF16, 4), "traffic": traffic,
+            "traffic_source": tsrc,
             "measured": "HIP events on the launch stream around each GEMM of the last CFG forward of the last timed step",
             "launches_per_forward": n, "avg_launch_ms": round(tot_t / n * 1e3, 4),
             "flops_per_launch": round(tot_f / n), "flops_per_forward": gemm_flops_per_forward(ncfg, rows)}

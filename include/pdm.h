@@ -37,8 +37,11 @@ extern "C" {
 const char* pdm_last_error(void);
 int pdm_version(void);
 int pdm_device_arch(char* buf, int len);
-/* GEMM tile policy (benchmarking / A-B): 0 = auto, 1 = 128x128 tile, 2 = 256x256 tile */
-int pdm_set_gemm_algo(int algo);   /* gcnArchName of the current device, e.g. "gfx950:sramecc+:xnack-" */
+/* Tile-policy overrides for A/B measurement (0 = automatic; the default everywhere).
+ *   GEMM: 1 = 128x128, 2 = 256x256 BK32 ring, 3 = 256x256 BK64 ring, 4 = 256x256 8-phase staggered
+ *   attention: 1 = streamed K/V per 64-query block, 2 / 3 = head-resident K/V with 2 / 3 query tiles per wave */
+int pdm_set_gemm_algo(int algo);
+int pdm_set_attention_algo(int algo);
 
 /* ---- network handle: libs/uvit.py:138-230 UViT, libs/uvit_t2i.py:258-525 UViT (t2i) -------------- */
 typedef struct pdm_uvit pdm_uvit;

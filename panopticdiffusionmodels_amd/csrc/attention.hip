@@ -191,6 +191,169 @@ __global__ __launch_bounds__(256) void attention_kernel(AttentionArgs p, int nqt
     }
   }
 }
+
+// ------------------------------------------------------------------------------------------------
+// Head-resident variant for Dh = 64 and L <= 640 (every U-ViT-L/M/S, CIFAR and t2i shape): one workgroup
+// per (b, h) stages the head's whole K and V (L x 128 B each, XOR-swizzled rows, no padding) into LDS with
+// LDS-DMA once, then every wave runs T query tiles of 16 over all keys with no further barrier.  K/V are
+// read from HBM once per head (not once per 64-query block), the 16-query tiles tile L with one ragged
+// tile, and each K / V^T fragment read from LDS feeds T MFMAs.
+//   K rows: 16-B chunk c stored at c ^ ((row >> 1) & 7)   (conflict-free ds_read_b128 fragment reads)
+//   V rows: 32-B unit u stored at u ^ ((row >> 1) & 3)    (conflict-free ds_read_b64_tr_b16 reads)
+// The softmax scale is folded into one FMA before exp2; key masking only runs in the last 64-key block.
+template <int T>
+__global__ __launch_bounds__(T == 2 ? 768 : 512) void attention_kv_kernel(AttentionArgs p, int nqt, int Lp) {
+  constexpr int DH = 64;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* Ks = lds;
+  char* Vs = lds + Lp * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int bh = blockIdx.x;
+  const int b = bh / p.H, h = bh % p.H;
+  const int L = p.L, D = p.H * DH;
+  const bf16* base = p.qkv + (size_t)b * L * p.ldq + h * DH;
+
+  // stage K and V: one wave-instruction = 8 rows x 128 B, lane -> (row = lane >> 3, physical chunk lane & 7)
+  {
+    const int r8 = lane >> 3, pc = lane & 7;
+    for (int grp = wave; grp < Lp / 8; grp += nw) {
+      const int row = grp * 8 + r8;
+      const int key = row < L ? row : L - 1;
+      const bf16* src = base + (size_t)key * p.ldq;
+      const int kc = pc ^ ((row >> 1) & 7);
+      const int vc = ((((pc >> 1) ^ ((row >> 1) & 3)) << 1) | (pc & 1));
+      glds16(src + D + kc * 8, (PDM_LDS void*)(Ks + grp * 1024));
+      glds16(src + 2 * D + vc * 8, (PDM_LDS void*)(Vs + grp * 1024));
+    }
+  }
+
+  const int g = lane >> 4, col = lane & 15;
+  // Q^T fragments of this wave's tiles (B operand): lane holds Q[q = tile*16 + col][d = ks*32 + g*8 .. +8]
+  bf16x8 qf[T][2];
+  bool tv[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int tile = wave + t * nw;
+    tv[t] = tile < nqt;
+    int q = tile * 16 + col;
+    q = q < L ? q : L - 1;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[t][ks] = *reinterpret_cast<const bf16x8*>(base + (size_t)q * p.ldq + ks * 32 + g * 8);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!tv[0]) return;
+
+  const float sl2 = p.scale * 1.4426950408889634f;
+  float m_run[T], l_run[T];
+  f32x4 acc[T][4];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    m_run[t] = -1e30f;
+    l_run[t] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int nch = (L + 63) / 64;
+  for (int c = 0; c < nch; ++c) {
+    const int kvalid = L - c * 64;           // keys of this block (>= 64 except in the last block)
+    f32x4 s[T][4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (kt * 16 < kvalid) {
+        const int row = c * 64 + kt * 16 + col;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + row * 128 + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 4));
+#pragma unroll
+          for (int t = 0; t < T; ++t)
+            if (t == 0 || tv[t]) s[t][kt] = mfma16x16x32(kf, qf[t][ks], s[t][kt]);
+        }
+      }
+    }
+    if (kvalid < 64) {   // ragged last block: mask keys >= L
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (kt * 16 + g * 4 + j >= kvalid)
+#pragma unroll
+            for (int t = 0; t < T; ++t) s[t][kt][j] = -INFINITY;
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      float cmax = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+        cmax = fmaxf(cmax, fmaxf(fmaxf(s[t][kt][0], s[t][kt][1]), fmaxf(s[t][kt][2], s[t][kt][3])));
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      const float m_new = fmaxf(m_run[t], cmax * sl2);
+      const float alpha = exp2f(m_run[t] - m_new);
+      m_run[t] = m_new;
+      float ls = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float e = exp2f(fmaf(s[t][kt][j], sl2, -m_new));
+          s[t][kt][j] = e;
+          ls += e;
+        }
+      l_run[t] = l_run[t] * alpha + ls;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[t][i] *= alpha;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (kk * 32 >= kvalid) break;
+      bf16x8 pf[T];
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pf[t][j] = (bf16)s[t][2 * kk][j];
+          pf[t][4 + j] = (bf16)s[t][2 * kk + 1][j];
+        }
+      const int qq = col >> 2, pp = col & 3;
+      const int r1 = c * 64 + kk * 32 + 4 * g + qq, r2 = r1 + 16;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const s16x4 lo = lds_read_tr16(Vs + r1 * 128 + ((dt ^ ((r1 >> 1) & 3)) << 5) + 8 * pp);
+        const s16x4 hi = lds_read_tr16(Vs + r2 * 128 + ((dt ^ ((r2 >> 1) & 3)) << 5) + 8 * pp);
+        const bf16x4 lob = __builtin_bit_cast(bf16x4, lo);
+        const bf16x4 hib = __builtin_bit_cast(bf16x4, hi);
+        bf16x8 vf;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { vf[j] = lob[j]; vf[4 + j] = hib[j]; }
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+          if (t == 0 || tv[t]) acc[t][dt] = mfma16x16x32(vf, pf[t], acc[t][dt]);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    if (!tv[t]) continue;
+    float l = l_run[t];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
+    const int q = (wave + t * nw) * 16 + col;
+    if (q < L) {
+      bf16* orow = p.out + ((size_t)b * L + q) * p.ldo + h * DH;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const f32x4 v = acc[t][dt] * inv;
+        *reinterpret_cast<bf16x4*>(orow + dt * 16 + g * 4) = to_bf16x4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
 }  // namespace
 
 const char* attention_check(const AttentionArgs& p) {
@@ -203,8 +366,31 @@ const char* attention_check(const AttentionArgs& p) {
   return nullptr;
 }
 
+static int g_attention_algo = 0;   // 0 auto, 1 = 64-query blocks with streamed K/V, 2/3 = head-resident T = 2/3
+void attention_set_algo(int algo) { g_attention_algo = algo; }
+
 hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream) {
   const int nqt = (p.L + 15) / 16;
+  int algo = g_attention_algo;
+  const int Lp = (p.L + 31) / 32 * 32;   // PV reads whole 32-key steps
+  if (p.Dh != 64 || Lp * 256 > 160 * 1024) algo = 1;
+  if (algo == 0) algo = (nqt + 1) / 2 <= 12 ? 2 : 3;
+  if (algo == 2 || algo == 3) {
+    const int T = algo;
+    const int nw = (nqt + T - 1) / T;
+    if (nw <= (T == 2 ? 12 : 8)) {
+      const int smem = Lp * 256;
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)attention_kv_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)attention_kv_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+      }
+      if (T == 2) hipLaunchKernelGGL(attention_kv_kernel<2>, dim3(p.B * p.H), dim3(nw * 64), smem, stream, p, nqt, Lp);
+      else hipLaunchKernelGGL(attention_kv_kernel<3>, dim3(p.B * p.H), dim3(nw * 64), smem, stream, p, nqt, Lp);
+      return hipGetLastError();
+    }
+  }
   const int nqb = (nqt + 3) / 4;
   const int nbh = p.B * p.H;
   dim3 grid(((nbh + 7) / 8) * 8 * nqb), block(256);

@@ -295,6 +295,12 @@ int pdm_set_gemm_algo(int algo) {
   return PDM_OK;
 }
 
+int pdm_set_attention_algo(int algo) {
+  if (algo < 0 || algo > 3) return fail(PDM_ERR_ARG, "pdm_set_attention_algo: algo must be 0 (auto), 1, 2 or 3");
+  pdm::attention_set_algo(algo);
+  return PDM_OK;
+}
+
 int pdm_device_arch(char* buf, int len) {
   int dev = 0;
   PDM_HIP(hipGetDevice(&dev));

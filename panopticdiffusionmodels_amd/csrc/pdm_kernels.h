@@ -62,6 +62,7 @@ struct AttentionArgs {
 };
 const char* attention_check(const AttentionArgs& p);
 hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream);
+void attention_set_algo(int algo);
 
 // Token assembly (libs/uvit.py:201-212, libs/uvit_t2i.py:382-409):
 // out[b, row] for the sequence [label?][time][context x n_ctx?][patches] + pos_embed, fp32.

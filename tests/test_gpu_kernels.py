@@ -120,6 +120,26 @@ def test_attention(lib, L, Dh):
     assert rel(out.float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("algo", [1, 2, 3])
+@pytest.mark.parametrize("L", [17, 66, 257, 258, 334, 590])
+def test_attention_algos(lib, algo, L):
+    """Both attention structures (1: streamed K/V per 64-query block; 2/3: head-resident K/V, 2 or 3 query
+    tiles per wave) at Dh = 64 on ragged lengths (the head-resident path declines shapes it cannot hold)."""
+    H, B, Dh = 4, 3, 64
+    D = H * Dh
+    g = torch.Generator(device="cuda").manual_seed(L + algo)
+    qkv = (torch.randn(B * L, 3 * D, device="cuda", generator=g) * 1.5).bfloat16()
+    lib.load().pdm_set_attention_algo(algo)
+    try:
+        out = lib.attention(qkv, B, L, H, Dh)
+    finally:
+        lib.load().pdm_set_attention_algo(0)
+    q, k, v = qkv.float().reshape(B, L, 3, H, Dh).permute(2, 0, 3, 1, 4)
+    ref = torch.softmax(q @ k.transpose(-1, -2) * Dh ** -0.5, dim=-1) @ v
+    ref = ref.permute(0, 2, 1, 3).reshape(B * L, D)
+    assert rel(out.float(), ref) < 1e-2
+
+
 def test_attention_spiky(lib):
     """A key row far above the rest forces a late running-max jump (online-softmax rescale branch)."""
     B, L, H, Dh = 1, 258, 2, 64
