@@ -166,6 +166,16 @@ int pdm_decoder_workspace_size(const pdm_decoder* d, int batch, size_t* bytes);
 int pdm_decoder_decode(pdm_decoder* d, const float* z, float* img, int batch, void* workspace,
                        size_t workspace_bytes, void* stream);
 
+/* ---- output stage (utils.sample2dir, utils.py:561-640) ------------------------------------------
+ * Decoded images fp32 [B, C, H, W] -> uint8 [B, H, W, C]: unpreprocess (datasets.py:104-108) followed by
+ * torchvision save_image's quantisation (v * 255 + 0.5, clamp, truncate), bit-exact. */
+int pdm_images_to_u8(const float* img, uint8_t* out, int B, int C, int H, int W, void* stream);
+/* Analog-bit masks fp32 [B, nbits, H, W] -> ids int32 [B, H, W] = bits2int(pred_mask > 0) (utils.py:490-518)
+ * and/or colour-mapped uint8 [B, H, W, 3] = colormap[id] (utils.py:532-543; colormap int32 [256][3]).
+ * Either output may be NULL (not both). */
+int pdm_mask_bits_to_rgb(const float* bits, int nbits, const int32_t* colormap, int32_t* ids, uint8_t* rgb, int B,
+                         int H, int W, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -79,6 +79,10 @@ _SIGS = {
     "pdm_attention": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p]),
     "pdm_f32_to_bf16": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]),
+    "pdm_images_to_u8": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_void_p]),
+    "pdm_mask_bits_to_rgb": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "pdm_decoder_create": (ctypes.c_int, [ctypes.POINTER(PdmDecoderCfg), ctypes.POINTER(ctypes.c_void_p)]),
     "pdm_decoder_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "pdm_decoder_param_count": (ctypes.c_int, [ctypes.c_void_p]),

@@ -1,0 +1,37 @@
+"""A/B timing of the attention structures on one U-ViT shape (dev tool, one process, interleaved rounds).
+python tools/attn_bench.py [rows L H Dh]"""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from panopticdiffusionmodels_amd import _lib  # noqa: E402
+
+rows, L, H, Dh = (int(v) for v in (sys.argv[1:5] if len(sys.argv) > 4 else (190, 258, 16, 64)))
+lib = _lib.load()
+g = torch.Generator(device="cuda").manual_seed(0)
+qkv = torch.randn(rows * L, 3 * H * Dh, device="cuda", generator=g).bfloat16()
+flops = 4.0 * rows * H * L * L * Dh
+algos = [1, 2, 3]
+outs = {}
+for a in algos:
+    lib.pdm_set_attention_algo(a)
+    outs[a] = _lib.attention(qkv, rows, L, H, Dh).float()
+err = max(float((outs[1] - outs[a]).norm() / outs[1].norm()) for a in algos)
+times = {a: [] for a in algos}
+for rnd in range(7):
+    for a in algos:
+        lib.pdm_set_attention_algo(a)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            _lib.attention(qkv, rows, L, H, Dh)
+        e1.record()
+        torch.cuda.synchronize()
+        times[a].append(e0.elapsed_time(e1) / 10)
+lib.pdm_set_attention_algo(0)
+line = f"attention rows={rows} L={L} H={H} Dh={Dh} maxrelerr={err:.1e}"
+for a in algos:
+    t = sorted(times[a])[3]
+    line += f" | algo{a} {t*1e3:8.1f} us {flops/t/1e9:7.1f} TF/s"
+print(line)
