@@ -702,7 +702,7 @@ static hipError_t launch8p(const GemmArgs& p, int epi, hipStream_t stream) {
 
 hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream) {
   int algo = g_gemm_algo;
-  if (algo == 0) algo = (p.M >= 4096 && p.N >= 512) ? 3 : 1;
+  if (algo == 0) algo = (p.M >= 4096 && p.N >= 256) ? 3 : 1;
   // the 256-tile bf16 epilogue stores 16-byte row chunks: needs N, ldo multiples of 8 and an aligned output
   if ((epi == EPI_BF16 || epi == EPI_GELU) && (p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))) algo = 1;
   if (epi == EPI_F32 && (p.N % 8 || p.ldr % 4 || ((uintptr_t)p.out_f32 & 15) ||
