@@ -39,9 +39,14 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const T* x, int P, int 
   const T* xb = x + (size_t)b * P * C;
   // thread -> 4 consecutive channels; lanes stride over channels, then pixels
   const int nq = C / 4;
-  double su[2] = {0.0, 0.0}, sq[2] = {0.0, 0.0};
-  int gsel[2] = {-1, -1};
-  for (int q = threadIdx.x % nq, k = 0; k < 2 && q < nq; q += 256, ++k) gsel[k] = (q * 4) / cpg;
+  // a quad of channels spans at most two groups (cpg = C/32 >= 2): accumulate lo/hi group separately
+  double su[2][2] = {{0.0, 0.0}, {0.0, 0.0}}, sq[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+  int glo[2] = {-1, -1}, ghi[2] = {-1, -1}, split[2] = {4, 4};
+  for (int q = threadIdx.x % nq, k = 0; k < 2 && q < nq; q += 256, ++k) {
+    glo[k] = (q * 4) / cpg;
+    ghi[k] = (q * 4 + 3) / cpg;
+    split[k] = (glo[k] + 1) * cpg - q * 4;   // channels j < split belong to glo
+  }
   const int plane = threadIdx.x / nq;          // pixel lane (C < 1024)
   const int planes = max(1, 256 / nq);
   for (int pi = p0 + plane; pi < p1; pi += planes) {
@@ -56,16 +61,22 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const T* x, int P, int 
         const bf16x4 t = *reinterpret_cast<const bf16x4*>(row + q * 4);
         v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
       }
-      const float s4 = (v[0] + v[1]) + (v[2] + v[3]);
-      const float q4 = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
-      su[k] += s4;
-      sq[k] += q4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = j >= split[k] ? 1 : 0;
+        su[k][h] += v[j];
+        sq[k][h] += v[j] * v[j];
+      }
     }
   }
   for (int k = 0; k < 2; ++k)
-    if (gsel[k] >= 0 && threadIdx.x < nq * planes) {
-      atomicAdd(&s_sum[gsel[k]], su[k]);
-      atomicAdd(&s_sq[gsel[k]], sq[k]);
+    if (glo[k] >= 0 && threadIdx.x < nq * planes) {
+      atomicAdd(&s_sum[glo[k]], su[k][0]);
+      atomicAdd(&s_sq[glo[k]], sq[k][0]);
+      if (ghi[k] != glo[k]) {
+        atomicAdd(&s_sum[ghi[k]], su[k][1]);
+        atomicAdd(&s_sq[ghi[k]], sq[k][1]);
+      }
     }
   __syncthreads();
   if (threadIdx.x < 32) {
@@ -106,8 +117,6 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* x, const float* 
     const long long pix = e / nq;
     const int b = (int)(pix / P);
     const int c = q * 4;
-    const int g = c / cpg;
-    const float mean = stats[(b * 32 + g) * 2], rstd = stats[(b * 32 + g) * 2 + 1];
     float v[4];
     if constexpr (sizeof(T) == 4) {
       const f32x4 t = *reinterpret_cast<const f32x4*>(x + pix * C + c);
@@ -119,6 +128,8 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* x, const float* 
     bf16x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+      const int g = (c + j) / cpg;   // cpg may be 2 or 6: a quad can straddle two groups
+      const float mean = stats[(b * 32 + g) * 2], rstd = stats[(b * 32 + g) * 2 + 1];
       float u = (v[j] - mean) * rstd * gamma[c + j] + beta[c + j];
       if (swish) u = u / (1.0f + __expf(-u));
       o[j] = (bf16)u;
