@@ -125,6 +125,15 @@ int pdm_lincomb(float* out, int n_terms, const float* const* T, const float* c, 
 int pdm_gemm_bf16(const void* A1, int lda1, const void* A2, int lda2, int K1, const void* W, const float* bias,
                   int M, int N, int K, int epi, void* out_bf16, int ldo, float* out_f32, int ldr, int accumulate,
                   void* stream);
+/* Implicit-GEMM conv3x3 (stride 1, pad 1) on NHWC bf16 input [B, H>>up, W>>up, Cin] (up = 1: the nearest-x2
+ * upsample of libs/autoencoder.py:35-50 folded into the addressing); Wt [N][9*Cin] in (ky, kx, ci) order;
+ * output rows = output pixels (b, y, x), N channels (libs/autoencoder.py ResnetBlock conv1/conv2, Upsample.conv) */
+int pdm_gemm_conv3x3_bf16(const void* in, int B, int H, int W, int Cin, int up, const void* Wt, const float* bias,
+                          int N, int epi, void* out_bf16, float* out_f32, int accumulate, void* stream);
+/* batch independent GEMMs (operand strides in elements; the decoder AttnBlock's q k^T and p v, autoencoder.py:177-188) */
+int pdm_gemm_batched_bf16(const void* A, int lda, long long sA, const void* W, int ldw, long long sW,
+                          const float* bias, int M, int N, int K, int batch, int epi, void* out_bf16, int ldo,
+                          long long sO, float* out_f32, int ldr, long long sR, int accumulate, void* stream);
 /* nn.LayerNorm (libs/uvit.py:100,103,180): fp32 rows -> bf16 rows */
 int pdm_layernorm(const float* x, int ldx, const float* gamma, const float* beta, void* y, int ldy, int rows, int D,
                   float eps, void* stream);

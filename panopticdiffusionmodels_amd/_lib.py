@@ -73,6 +73,14 @@ _SIGS = {
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_void_p]),
+    "pdm_gemm_conv3x3_bf16": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "pdm_gemm_batched_bf16": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p,
+                                             ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                             ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_int,
+                                             ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p]),
     "pdm_layernorm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                      ctypes.c_void_p]),
@@ -160,6 +168,39 @@ def gemm(a, w, bias=None, epi=EPI_BF16, out=None, out_f32=None, accumulate=False
                             ptr(out_f32), out_f32.stride(0) if out_f32 is not None else 0, int(accumulate),
                             stream_ptr(a.device)), "pdm_gemm_bf16")
     return out_f32 if epi == EPI_F32 else out
+
+
+def gemm_conv3x3(x, w, bias=None, epi=EPI_F32, up=0, out=None, out_f32=None, accumulate=False):
+    """Implicit-GEMM conv3x3 (pad 1) on NHWC bf16 x [B, h, w, Cin]; w [N, Cin, 3, 3] bf16 (torch layout, repacked
+    here to the kernel's (ky, kx, ci) K order).  up=1 convolves the nearest-x2 upsample of x."""
+    lib = load()
+    require_gpu(x)
+    B, h, wd, C = x.shape
+    H, W = h << up, wd << up
+    N = w.shape[0]
+    wk = w.permute(0, 2, 3, 1).reshape(N, 9 * C).contiguous()
+    if epi in (EPI_BF16, EPI_GELU) and out is None:
+        out = torch.empty(B * H * W, N, dtype=torch.bfloat16, device=x.device)
+    if epi == EPI_F32 and out_f32 is None:
+        out_f32 = torch.zeros(B * H * W, N, dtype=torch.float32, device=x.device)
+    check(lib.pdm_gemm_conv3x3_bf16(ptr(x), B, H, W, C, up, ptr(wk), ptr(bias), N, epi, ptr(out), ptr(out_f32),
+                                    int(accumulate), stream_ptr(x.device)), "pdm_gemm_conv3x3_bf16")
+    return out_f32 if epi == EPI_F32 else out
+
+
+def gemm_batched(a, w, bias=None, epi=EPI_F32):
+    """out[z] = a[z] @ w[z].T (+ bias) for a [Z, M, K], w [Z, N, K] bf16 contiguous."""
+    lib = load()
+    require_gpu(a)
+    Z, M, K = a.shape
+    N = w.shape[1]
+    if epi == EPI_F32:
+        ob, of = None, torch.zeros(Z, M, N, dtype=torch.float32, device=a.device)
+    else:
+        ob, of = torch.empty(Z, M, N, dtype=torch.bfloat16, device=a.device), None
+    check(lib.pdm_gemm_batched_bf16(ptr(a), K, M * K, ptr(w), K, N * K, ptr(bias), M, N, K, Z, epi, ptr(ob), N, M * N,
+                                    ptr(of), N, M * N, 0, stream_ptr(a.device)), "pdm_gemm_batched_bf16")
+    return of if epi == EPI_F32 else ob
 
 
 def layernorm(x, gamma, beta, eps=1e-5):

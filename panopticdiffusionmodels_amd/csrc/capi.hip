@@ -290,7 +290,7 @@ const char* pdm_last_error(void) { return g_err.c_str(); }
 int pdm_version(void) { return 1; }
 
 int pdm_set_gemm_algo(int algo) {
-  if (algo < 0 || algo > 4) return fail(PDM_ERR_ARG, "pdm_set_gemm_algo: algo must be 0 (auto), 1, 2, 3 or 4");
+  if (algo < 0 || algo > 7) return fail(PDM_ERR_ARG, "pdm_set_gemm_algo: algo must be 0 (auto) or 1..7");
   pdm::gemm_set_algo(algo);
   return PDM_OK;
 }
@@ -633,6 +633,43 @@ int pdm_gemm_bf16(const void* A1, int lda1, const void* A2, int lda2, int K1, co
   a.out_bf16 = (bf16*)out_bf16; a.ldo = ldo;
   a.out_f32 = out_f32; a.ldr = ldr;
   a.accumulate = accumulate;
+  PDM_CHECK(pdm::gemm_check(a, epi));
+  PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_gemm_conv3x3_bf16(const void* in, int B, int H, int W, int Cin, int up, const void* Wt, const float* bias,
+                          int N, int epi, void* out_bf16, float* out_f32, int accumulate, void* stream) {
+  static bf16* zero = nullptr;   // zero page for the tile policies that address padded taps explicitly
+  if (!zero) {
+    PDM_HIP(hipMalloc(&zero, 4096));
+    PDM_HIP(hipMemset(zero, 0, 4096));
+  }
+  pdm::GemmArgs a{};
+  a.A1 = (const bf16*)in; a.lda1 = Cin; a.K1 = 9 * Cin;
+  a.W = (const bf16*)Wt; a.bias = bias;
+  a.M = B * H * W; a.N = N; a.K = 9 * Cin;
+  a.out_bf16 = (bf16*)out_bf16; a.ldo = N;
+  a.out_f32 = out_f32; a.ldr = N;
+  a.accumulate = accumulate;
+  a.conv = 1; a.convH = H; a.convW = W; a.convC = Cin; a.conv_up = up; a.zero = zero;
+  PDM_CHECK(pdm::gemm_check(a, epi));
+  PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_gemm_batched_bf16(const void* A, int lda, long long sA, const void* W, int ldw, long long sW,
+                          const float* bias, int M, int N, int K, int batch, int epi, void* out_bf16, int ldo,
+                          long long sO, float* out_f32, int ldr, long long sR, int accumulate, void* stream) {
+  pdm::GemmArgs a{};
+  a.A1 = (const bf16*)A; a.lda1 = lda; a.K1 = K;
+  a.W = (const bf16*)W; a.ldw = ldw; a.bias = bias;
+  a.M = M; a.N = N; a.K = K;
+  a.out_bf16 = (bf16*)out_bf16; a.ldo = ldo;
+  a.out_f32 = out_f32; a.ldr = ldr;
+  a.accumulate = accumulate;
+  a.batch = batch; a.sA = sA; a.sW = sW; a.sO = sO; a.sR = sR;
+  if (batch < 1) return fail(PDM_ERR_ARG, "pdm_gemm_batched_bf16: batch must be >= 1");
   PDM_CHECK(pdm::gemm_check(a, epi));
   PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
   return PDM_OK;

@@ -272,8 +272,8 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
       *reinterpret_cast<f32x4*>(smem + ml * 1024 + (((nl >> 2) ^ (ml & 63)) << 4)) = acc[f];
     }
     __syncthreads();
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
+#pragma unroll 1
+    for (int g = 0; g < 2; ++g) {   // not unrolled: keeps the staged rows + residual loads within the VGPR budget
       f32x4 v0[4], v1[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -626,6 +626,277 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs p, int tiles_n,
 
   epilogue256<EPI, 1>(p, acc, smem, m0, n0, tid, lane, wm, wn);
 }
+
+// ------------------------------------------------------------------------------------------------
+// 256x256x64 tile, 8 waves, 8-phase schedule with a deep LDS-DMA pipeline (algo 5).
+// Same quadrant decomposition and stagger as gemm8p_kernel, but every half-tile slot is refilled as soon as
+// its last fragment read is two phases old, so four half-tiles (8 LDS-DMA per wave) stay in flight and each
+// half-tile has four phases (~2k cycles) to land instead of one or two:
+//   phase (reads)        issues           waits for (vmcnt 8 in steady state)
+//   P1 q(0,0) (A0, W0)   W1 of tile k+1   W1(k)
+//   P2 q(0,1) (W1)       A1 of tile k+1   A1(k)
+//   P3 q(1,1) (A1)       A0 of tile k+2   -
+//   P4 q(1,0) (-)        W0 of tile k+2   A0(k+1), W0(k+1)
+// Operands are addressed through buffer descriptors (32-bit per-lane offsets, K offset in the scalar
+// offset): rows past M / N and padded conv taps take an out-of-range offset and the hardware returns zeros,
+// so neither tail clamping nor a zero page is needed.
+constexpr unsigned OOB = 0x80000000u;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff, PDM_LDS void* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds, 16, (int)voff, soff, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
+  const unsigned n = bytes >= 0x7fffffffLL ? 0x7fffffffu : (unsigned)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)n, 0x00020000);
+}
+
+template <int EPI, int CONV, int SCHED>
+__global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n, int nwg) {
+  constexpr int ROWB = 128;
+  constexpr int HALF = 128 * ROWB;              // 16 KiB half-tile
+  constexpr int BUF = 4 * HALF;                 // A0 A1 W0 W1
+  enum { KA0 = 0, KA1 = 1, KW0 = 2, KW1 = 3 };
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+  }
+  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  if (p.batch > 1) {
+    const long long z = blockIdx.y;
+    p.A1 += z * p.sA;
+    p.W += z * p.sW;
+    if (p.out_bf16) p.out_bf16 += z * p.sO;
+    if (p.out_f32) p.out_f32 += z * p.sR;
+  }
+  const int ldw = p.ldw > 0 ? p.ldw : p.K;
+
+  // descriptor extents (bytes) of the three operands
+  long long a1_rows;
+  if (CONV) a1_rows = (long long)(p.M / (p.convH * p.convW)) * (p.convH >> p.conv_up) * (p.convW >> p.conv_up);
+  else if (p.a_rows_per_group > 0)
+    a1_rows = (long long)((p.M - 1) / p.a_rows_per_group) * p.a_group_stride + p.a_rows_per_group;
+  else a1_rows = p.M;
+  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(p.A1, a1_rows * (CONV ? p.convC : p.lda1) * 2);
+  const __amdgpu_buffer_rsrc_t ra2 = make_rsrc(p.A2 ? p.A2 : p.A1, p.A2 ? (long long)p.M * p.lda2 * 2 : 0);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.W, (long long)(p.N - 1) * ldw * 2 + (long long)p.K * 2);
+
+  // per-lane offsets of this wave's two 1 KiB pieces (8 rows x 128 B) in each half (h) of A and W
+  const int prow = lane >> 3, pch = lane & 7;
+  unsigned a1off[2][2], a2off[2][2], woff[2][2];
+  int cpix[2][2];   // conv: (b * H + y) << 12 | x of the piece row's output pixel, -1 past M
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + prow;
+    const unsigned sb = (unsigned)((pch ^ ((row >> 1) & 7)) * 16);   // logical chunk stored at physical pch
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int gm = m0 + h * 128 + row;
+      if constexpr (CONV) {
+        if (gm < p.M) {
+          const int hw = p.convH * p.convW, b = gm / hw, r = gm - b * hw, y = r / p.convW;
+          cpix[h][i] = ((b * p.convH + y) << 12) | (r - y * p.convW);
+        } else {
+          cpix[h][i] = -1;
+        }
+        a1off[h][i] = sb;
+        a2off[h][i] = 0;
+      } else {
+        const int gm1 = p.a_rows_per_group > 0 ? (gm / p.a_rows_per_group) * p.a_group_stride + gm % p.a_rows_per_group : gm;
+        a1off[h][i] = gm < p.M ? (unsigned)gm1 * (unsigned)(p.lda1 * 2) + sb : OOB;
+        a2off[h][i] = gm < p.M ? (unsigned)gm * (unsigned)(p.lda2 * 2) + sb : OOB;
+        cpix[h][i] = 0;
+      }
+      const int gn = n0 + h * 128 + row;
+      woff[h][i] = gn < p.N ? (unsigned)gn * (unsigned)(ldw * 2) + sb : OOB;
+    }
+  }
+
+  auto issue = [&](int kt, int kind) {
+    const int k0 = kt * 64;
+    char* dst = smem + (kt & 1) * BUF + kind * HALF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      PDM_LDS void* d = (PDM_LDS void*)(dst + (wave * 2 + i) * 1024);
+      if (kind >= KW0) {
+        dma16(rw, woff[kind - KW0][i], k0 * 2, d);
+      } else if constexpr (CONV) {
+        const int tap = k0 / p.convC, ci0 = k0 - tap * p.convC;
+        const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+        const int pix = cpix[kind][i];
+        const int yy = ((pix >> 12) % p.convH) + dy, xx = (pix & 4095) + dx;
+        const int bb = (pix >> 12) / p.convH;
+        unsigned off = OOB;
+        if (pix >= 0 && yy >= 0 && yy < p.convH && xx >= 0 && xx < p.convW) {
+          const int sh = p.conv_up, Hs = p.convH >> sh, Ws = p.convW >> sh;
+          off = (unsigned)(((bb * Hs + (yy >> sh)) * Ws + (xx >> sh)) * p.convC) * 2u + a1off[kind][i];
+        }
+        dma16(ra1, off, ci0 * 2, d);
+      } else {
+        if (k0 < p.K1) dma16(ra1, a1off[kind][i], k0 * 2, d);
+        else dma16(ra2, a2off[kind][i], (k0 - p.K1) * 2, d);
+      }
+    }
+  };
+
+  f32x4 acc[32];
+#pragma unroll
+  for (int f = 0; f < 32; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2];      // A fragments of the current A half: [mi][k-sub]
+  bf16x8 wf[2][2][2];   // W fragments of both W halves: [qj][ni][k-sub]
+
+  auto read_a = [&](const char* buf, int qi) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int row = wm * 64 + mi * 16 + (lane & 15);
+        af[mi][ks] = *reinterpret_cast<const bf16x8*>(buf + qi * HALF + swz_off<64>(row, ks * 4 + (lane >> 4)));
+      }
+  };
+  auto read_w = [&](const char* buf, int qj) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int row = wn * 32 + ni * 16 + (lane & 15);
+        wf[qj][ni][ks] = *reinterpret_cast<const bf16x8*>(buf + (2 + qj) * HALF + swz_off<64>(row, ks * 4 + (lane >> 4)));
+      }
+  };
+  // SCHED 1/2: the fragment reads of a phase are retired before its first barrier, so the MFMAs start on
+  // data already in registers and a slot is free for refill one phase after its last read.
+  auto lds_done = [&]() {
+    if constexpr (SCHED != 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto mma = [&](int qi, int qj) {
+    if constexpr (SCHED == 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          f32x4& c = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
+          c = mfma16x16x32(wf[qj][ni][ks], af[mi][ks], c);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = p.K / 64;
+  if constexpr (SCHED == 2) {
+    // 2 phases per K-tile: A (reads A0 W0 W1, quadrants (0,0) (0,1)) and B (reads A1, quadrants (1,0) (1,1)),
+    // 32 MFMAs each.  Issue order: A0 W0 W1 of tile k+2 in B(k), A1 of tile k+1 in A(k); every wait leaves
+    // the 8 youngest LDS-DMA (4 half-tiles) in flight.
+    issue(0, KA0);
+    issue(0, KW0);
+    issue(0, KW1);
+    issue(0, KA1);
+    if (nk > 1) {
+      issue(1, KA0);
+      issue(1, KW0);
+      issue(1, KW1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
+    bar_raw();
+    if (wave >= 4) bar_raw();
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* buf = smem + (kt & 1) * BUF;
+      const bool m1 = kt + 1 < nk, m2 = kt + 2 < nk;
+      // phase A
+      read_a(buf, 0);
+      read_w(buf, 0);
+      read_w(buf, 1);
+      lds_done();
+      if (m1) { issue(kt + 1, KA1); asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }   // A1(kt)
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar_raw();
+      mma(0, 0);
+      mma(0, 1);
+      bar_raw();
+      // phase B
+      read_a(buf, 1);
+      lds_done();
+      if (m2) {
+        issue(kt + 2, KA0);
+        issue(kt + 2, KW0);
+        issue(kt + 2, KW1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // A0 W0 W1 (kt+1)
+      } else if (m1) {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      bar_raw();
+      mma(1, 0);
+      mma(1, 1);
+      bar_raw();
+    }
+  } else {
+    issue(0, KA0);
+    issue(0, KW0);
+    issue(0, KW1);
+    issue(0, KA1);
+    if (nk > 1) {
+      issue(1, KA0);
+      issue(1, KW0);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    bar_raw();
+    if (wave >= 4) bar_raw();                            // stagger: waves 4-7 one barrier behind
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* buf = smem + (kt & 1) * BUF;
+      const bool m1 = kt + 1 < nk, m2 = kt + 2 < nk;
+      // P1: quadrant (0,0)
+      read_a(buf, 0);
+      read_w(buf, 0);
+      lds_done();
+      if (m1) { issue(kt + 1, KW1); asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      bar_raw();
+      mma(0, 0);
+      bar_raw();
+      // P2: quadrant (0,1)
+      read_w(buf, 1);
+      lds_done();
+      if (m1) { issue(kt + 1, KA1); asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar_raw();
+      mma(0, 1);
+      bar_raw();
+      // P3: quadrant (1,1)
+      read_a(buf, 1);
+      lds_done();
+      if (m2) issue(kt + 2, KA0);
+      bar_raw();
+      mma(1, 1);
+      bar_raw();
+      // P4: quadrant (1,0) on fragments already in registers
+      if (m2) { issue(kt + 2, KW0); asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+      else if (m1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      bar_raw();
+      mma(1, 0);
+      bar_raw();
+    }
+  }
+  if (wave < 4) bar_raw();                             // rejoin the stagger
+
+  epilogue256<EPI, 1>(p, acc, smem, m0, n0, tid, lane, wm, wn);
+}
 }  // namespace
 
 const char* gemm_check(const GemmArgs& p, int epi) {
@@ -700,6 +971,40 @@ static hipError_t launch8p(const GemmArgs& p, int epi, hipStream_t stream) {
   return hipGetLastError();
 }
 
+template <int CONV, int SCHED>
+static hipError_t launch8d(const GemmArgs& p, int epi, hipStream_t stream) {
+  constexpr int SMEM = 2 * 4 * 128 * 128;   // 128 KiB
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm8d_kernel<EPI_BF16, CONV, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8d_kernel<EPI_GELU, CONV, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8d_kernel<EPI_F32, CONV, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr_set = true;
+  }
+  const int tn = (p.N + BN2 - 1) / BN2, tm = (p.M + BM2 - 1) / BM2;
+  const int nwg = tm * tn;
+  dim3 grid(nwg, p.batch > 1 ? p.batch : 1), block(512);
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL((gemm8d_kernel<EPI_BF16, CONV, SCHED>), grid, block, SMEM, stream, p, tn, nwg); break;
+    case EPI_GELU: hipLaunchKernelGGL((gemm8d_kernel<EPI_GELU, CONV, SCHED>), grid, block, SMEM, stream, p, tn, nwg); break;
+    default: hipLaunchKernelGGL((gemm8d_kernel<EPI_F32, CONV, SCHED>), grid, block, SMEM, stream, p, tn, nwg); break;
+  }
+  return hipGetLastError();
+}
+
+// The descriptor-addressed kernel needs every operand byte offset below 2^31 (32-bit per-lane offsets).
+static bool fits_rsrc(const GemmArgs& p) {
+  const long long lim = 0x7fffffffLL;
+  long long a1;
+  if (p.conv) a1 = (long long)(p.M / (p.convH * p.convW)) * (p.convH >> p.conv_up) * (p.convW >> p.conv_up) * p.convC * 2;
+  else if (p.a_rows_per_group > 0)
+    a1 = ((long long)((p.M - 1) / p.a_rows_per_group) * p.a_group_stride + p.a_rows_per_group) * p.lda1 * 2;
+  else a1 = (long long)p.M * p.lda1 * 2;
+  const long long a2 = p.A2 ? (long long)p.M * p.lda2 * 2 : 0;
+  const long long w = (long long)p.N * (p.ldw > 0 ? p.ldw : p.K) * 2;
+  return a1 < lim && a2 < lim && w < lim && (!p.conv || p.convW < 4096);
+}
+
 hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream) {
   int algo = g_gemm_algo;
   if (algo == 0) algo = (p.M >= 4096 && p.N >= 256) ? 3 : 1;
@@ -707,6 +1012,12 @@ hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream) {
   if ((epi == EPI_BF16 || epi == EPI_GELU) && (p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))) algo = 1;
   if (epi == EPI_F32 && (p.N % 8 || p.ldr % 4 || ((uintptr_t)p.out_f32 & 15) ||
                          (p.out_bf16 && (p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))))) algo = 1;
+  if (algo >= 5 && fits_rsrc(p)) {
+    if (algo == 5) return p.conv ? launch8d<1, 0>(p, epi, stream) : launch8d<0, 0>(p, epi, stream);
+    if (algo == 6) return p.conv ? launch8d<1, 1>(p, epi, stream) : launch8d<0, 1>(p, epi, stream);
+    return p.conv ? launch8d<1, 2>(p, epi, stream) : launch8d<0, 2>(p, epi, stream);
+  }
+  if (algo >= 5) algo = 3;
   if (algo == 2 && p.K % 32 == 0) return launch256<32, 4>(p, epi, stream);
   if (algo == 4 && p.K % 128 == 0) return p.conv ? launch8p<1>(p, epi, stream) : launch8p<0>(p, epi, stream);
   if ((algo == 3 || algo == 4) && p.K % 64 == 0) return launch256<64, 2>(p, epi, stream);

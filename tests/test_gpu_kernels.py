@@ -59,17 +59,19 @@ def test_gemm_split_k(lib):
     assert rel(out, ref) < 2e-3
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4])
-@pytest.mark.parametrize("M,N,K", [(4133, 1000, 1024), (515, 768, 2048), (8192, 512, 128)])
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("M,N,K", [(4133, 1000, 1024), (515, 768, 2048), (8192, 512, 128), (700, 264, 64),
+                                   (1100, 520, 192)])
 @pytest.mark.parametrize("epi", ["gelu", "f32acc_copy", "split"])
 def test_gemm_algos(lib, algo, M, N, K, epi):
-    """Every tile policy (1: 128x128, 2/3: 256x256 ring, 4: 256x256 8-phase staggered) on ragged M/N tails."""
+    """Every tile policy (1: 128x128, 2/3: 256x256 ring, 4: 256x256 8-phase staggered, 5: 8-phase with the deep
+    descriptor-addressed LDS-DMA pipeline) on ragged M/N tails and short / odd K-tile counts."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K + algo)
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
     bias = torch.randn(N, device="cuda", generator=g)
     ref = a.float() @ w.float().t() + bias
-    lib.load().pdm_set_gemm_algo(algo)
+    lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
     try:
         if epi == "gelu":
             out = lib.gemm(a, w, bias, lib.EPI_GELU)
@@ -81,9 +83,60 @@ def test_gemm_algos(lib, algo, M, N, K, epi):
             assert rel(out, ref + r0) < 2e-3
             assert rel(cp.float(), ref + r0) < 1e-2
         else:
-            h = K // 2
-            out = lib.gemm(a[:, :h].contiguous(), w, bias, lib.EPI_F32, a2=a[:, h:].contiguous())
+            h = (K // 128) * 64 if K >= 128 else K   # split point on a 64-column boundary; K = 64 runs unsplit
+            a2 = a[:, h:].contiguous() if h < K else None
+            out = lib.gemm(a[:, :h].contiguous(), w, bias, lib.EPI_F32, a2=a2)
             assert rel(out, ref) < 2e-3
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+
+
+@pytest.mark.parametrize("algo", [1, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("B,h,Cin,N,up,epi", [(2, 16, 64, 128, 0, "f32acc"), (1, 8, 128, 256, 1, "f32"),
+                                              (3, 12, 64, 64, 0, "bf16"), (1, 32, 256, 256, 0, "f32"),
+                                              (2, 8, 128, 4, 0, "f32")])
+def test_gemm_conv3x3(lib, algo, B, h, Cin, N, up, epi):
+    """Implicit-GEMM conv3x3 mode (decoder ResnetBlock / Upsample convs, libs/autoencoder.py:35-50,110-141) for
+    every tile policy: ragged M (B*H*W not a tile multiple), the folded nearest-x2 upsample and the residual
+    accumulate, against F.conv2d on the same bf16 operands."""
+    g = torch.Generator(device="cuda").manual_seed(B * 100 + h + Cin + N + up + algo)
+    x = torch.randn(B, h, h, Cin, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, Cin, 3, 3, device="cuda", generator=g) * (9 * Cin) ** -0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    xin = x.float().permute(0, 3, 1, 2)
+    if up:
+        xin = F.interpolate(xin, scale_factor=2.0, mode="nearest")
+    ref = F.conv2d(xin, w.float(), bias, padding=1).permute(0, 2, 3, 1).reshape(-1, N)
+    lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
+    try:
+        if epi == "bf16":
+            out = lib.gemm_conv3x3(x, w, bias, lib.EPI_BF16, up=up)
+            assert rel(out.float(), ref) < 1e-2
+        elif epi == "f32":
+            out = lib.gemm_conv3x3(x, w, bias, lib.EPI_F32, up=up)
+            assert rel(out, ref) < 2e-3
+        else:
+            r0 = torch.randn(ref.shape, device="cuda", generator=g)
+            out = lib.gemm_conv3x3(x, w, bias, lib.EPI_F32, up=up, out_f32=r0.clone(), accumulate=True)
+            assert rel(out, ref + r0) < 2e-3
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+
+
+@pytest.mark.parametrize("algo", [1, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("Z,M,N,K", [(2, 1024, 1024, 512), (3, 300, 260, 128), (1, 4096, 512, 64)])
+def test_gemm_batched(lib, algo, Z, M, N, K):
+    """Batched operands (decoder AttnBlock q k^T and p v, libs/autoencoder.py:177-188) vs torch.bmm."""
+    g = torch.Generator(device="cuda").manual_seed(Z + M + N + K + algo)
+    a = torch.randn(Z, M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(Z, N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+    ref = torch.bmm(a.float(), w.float().transpose(1, 2))
+    lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
+    try:
+        out = lib.gemm_batched(a, w, None, lib.EPI_F32)
+        assert rel(out, ref) < 2e-3
+        outb = lib.gemm_batched(a, w, None, lib.EPI_BF16)
+        assert rel(outb.float(), ref) < 1e-2
     finally:
         lib.load().pdm_set_gemm_algo(0)
 
@@ -129,7 +182,7 @@ def test_attention_algos(lib, algo, L):
     D = H * Dh
     g = torch.Generator(device="cuda").manual_seed(L + algo)
     qkv = (torch.randn(B * L, 3 * D, device="cuda", generator=g) * 1.5).bfloat16()
-    lib.load().pdm_set_attention_algo(algo)
+    lib.check(lib.load().pdm_set_attention_algo(algo), "pdm_set_attention_algo")
     try:
         out = lib.attention(qkv, B, L, H, Dh)
     finally:

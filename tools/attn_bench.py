@@ -15,13 +15,13 @@ flops = 4.0 * rows * H * L * L * Dh
 algos = [1, 2, 3]
 outs = {}
 for a in algos:
-    lib.pdm_set_attention_algo(a)
+    assert lib.pdm_set_attention_algo(a) == 0, lib.pdm_last_error()
     outs[a] = _lib.attention(qkv, rows, L, H, Dh).float()
 err = max(float((outs[1] - outs[a]).norm() / outs[1].norm()) for a in algos)
 times = {a: [] for a in algos}
 for rnd in range(7):
     for a in algos:
-        lib.pdm_set_attention_algo(a)
+        assert lib.pdm_set_attention_algo(a) == 0, lib.pdm_last_error()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(10):

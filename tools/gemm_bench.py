@@ -26,14 +26,14 @@ for name, N, K, epi in shapes:
     a = A[:, :K].contiguous()
     outs = {}
     for algo in ALGOS:
-        lib.pdm_set_gemm_algo(algo)
+        assert lib.pdm_set_gemm_algo(algo) == 0, lib.pdm_last_error()
         o = _lib.gemm(a, W, bias, epi, out=None if epi != _lib.EPI_F32 else None)
         outs[algo] = o.float()
     err = max(float((outs[ALGOS[0]] - outs[x]).norm() / outs[ALGOS[0]].norm()) for x in ALGOS)
     times = {a: [] for a in ALGOS}
     for rnd in range(5):
         for algo in ALGOS:
-            lib.pdm_set_gemm_algo(algo)
+            assert lib.pdm_set_gemm_algo(algo) == 0, lib.pdm_last_error()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(10):

@@ -9,7 +9,7 @@ from panopticdiffusionmodels_amd import _lib  # noqa: E402
 algo, M, N, K, epi = (int(v) for v in sys.argv[1:6])
 iters = int(sys.argv[6]) if len(sys.argv) > 6 else 20
 lib = _lib.load()
-lib.pdm_set_gemm_algo(algo)
+assert lib.pdm_set_gemm_algo(algo) == 0, lib.pdm_last_error()
 g = torch.Generator(device="cuda").manual_seed(0)
 a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
 w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()

@@ -18,8 +18,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    n = name.split("(")[0].replace("void ", "")
-    return n.replace("pdm::(anonymous namespace)::", "")
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0].replace("pdm::", "")
 
 
 def per_kernel(path, counter):
@@ -27,7 +27,7 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        k = short(r["Kernel_Name"])
+        k = short(r["Kernel_Name"]) + f" grid={r['Grid_Size']}"
         acc[k][0] += float(r["Counter_Value"])
         acc[k][1] += 1
     return {k: (v[0] / v[1], v[1]) for k, v in acc.items()}
