@@ -125,6 +125,16 @@ int pdm_lincomb(float* out, int n_terms, const float* const* T, const float* c, 
 int pdm_gemm_bf16(const void* A1, int lda1, const void* A2, int lda2, int K1, const void* W, const float* bias,
                   int M, int N, int K, int epi, void* out_bf16, int ldo, float* out_f32, int ldr, int accumulate,
                   void* stream);
+/* Fused LayerNorm GEMM (libs/uvit.py:100,103 norm1 -> qkv, norm2 -> fc1).  Producer (epi = fp32, stats_out
+ * non-null): per row and 256-column group t, (sum, M2 about the group mean) of the stored fp32 values ->
+ * stats_out[row][ceil(N/256)][2].  Consumer (epi = bf16 / GELU, ln_stats non-null): A = bf16(x) un-normalised,
+ * W = W_ref * diag(norm.weight), ln_colsum[n] = sum_k W[n][k], bias = W_ref norm.bias (+ b_ref):
+ *   out = rstd * (A W^T - mean * ln_colsum) + bias,  mean / rstd merged from the row's ceil(K/256) partials. */
+int pdm_gemm_bf16_ln(const void* A, int lda, const void* W, const float* bias, int M, int N, int K, int epi,
+                     void* out_bf16, int ldo, float* out_f32, int ldr, int accumulate, float* stats_out,
+                     const float* ln_stats, const float* ln_colsum, float ln_eps, void* stream);
+/* LayerNorm partials of fp32 rows (as above) + optional bf16 copy xb [rows][D] */
+int pdm_rowstats(const float* x, int ldx, int rows, int D, void* xb, float* stats, void* stream);
 /* Implicit-GEMM conv3x3 (stride 1, pad 1) on NHWC bf16 input [B, H>>up, W>>up, Cin] (up = 1: the nearest-x2
  * upsample of libs/autoencoder.py:35-50 folded into the addressing); Wt [N][9*Cin] in (ky, kx, ci) order;
  * output rows = output pixels (b, y, x), N channels (libs/autoencoder.py ResnetBlock conv1/conv2, Upsample.conv) */

@@ -73,6 +73,12 @@ _SIGS = {
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_void_p]),
+    "pdm_gemm_bf16_ln": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p]),
+    "pdm_rowstats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p]),
     "pdm_gemm_conv3x3_bf16": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
@@ -168,6 +174,38 @@ def gemm(a, w, bias=None, epi=EPI_BF16, out=None, out_f32=None, accumulate=False
                             ptr(out_f32), out_f32.stride(0) if out_f32 is not None else 0, int(accumulate),
                             stream_ptr(a.device)), "pdm_gemm_bf16")
     return out_f32 if epi == EPI_F32 else out
+
+
+def rowstats(x, want_bf16=True):
+    """(bf16 copy, LayerNorm partials [rows, ceil(D/256), 2]) of fp32 rows x [rows, D]."""
+    lib = load()
+    require_gpu(x)
+    rows, D = x.shape
+    st = torch.empty(rows, (D + 255) // 256, 2, dtype=torch.float32, device=x.device)
+    xb = torch.empty(rows, D, dtype=torch.bfloat16, device=x.device) if want_bf16 else None
+    check(lib.pdm_rowstats(ptr(x), x.stride(0), rows, D, ptr(xb), ptr(st), stream_ptr(x.device)), "pdm_rowstats")
+    return xb, st
+
+
+def gemm_ln(a, w, bias, epi, ln_stats=None, ln_colsum=None, out=None, out_f32=None, accumulate=False,
+            stats_out=False, eps=1e-5):
+    """GEMM with the fused-LayerNorm operands (see include/pdm.h pdm_gemm_bf16_ln).  Returns the output, plus
+    the produced partials when stats_out."""
+    lib = load()
+    require_gpu(a)
+    M, K = a.shape
+    N = w.shape[0]
+    if epi in (EPI_BF16, EPI_GELU) and out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    if epi == EPI_F32 and out_f32 is None:
+        out_f32 = torch.zeros(M, N, dtype=torch.float32, device=a.device)
+    st = torch.empty(M, (N + 255) // 256, 2, dtype=torch.float32, device=a.device) if stats_out else None
+    check(lib.pdm_gemm_bf16_ln(ptr(a), a.stride(0), ptr(w), ptr(bias), M, N, K, epi, ptr(out),
+                               out.stride(0) if out is not None else 0, ptr(out_f32),
+                               out_f32.stride(0) if out_f32 is not None else 0, int(accumulate), ptr(st),
+                               ptr(ln_stats), ptr(ln_colsum), eps, stream_ptr(a.device)), "pdm_gemm_bf16_ln")
+    res = out_f32 if epi == EPI_F32 else out
+    return (res, st) if stats_out else res
 
 
 def gemm_conv3x3(x, w, bias=None, epi=EPI_F32, up=0, out=None, out_f32=None, accumulate=False):

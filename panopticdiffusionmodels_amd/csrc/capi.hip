@@ -77,17 +77,18 @@ struct pdm_uvit {
   const float* f(const std::string& name) const { return static_cast<const float*>(ptr(name)); }
   const bf16* w(const std::string& name) const { return static_cast<const bf16*>(ptr(name)); }
 
+  // norm1 / norm2 are folded into the next Linear (fused LayerNorm, see GemmArgs): the registered
+  // attn.qkv.weight / mlp.fc1.weight are W * diag(norm.weight) in bf16, ln_colsum their row sums and ln_bias
+  // W norm.bias (+ the Linear's own bias), both fp32 (include/pdm.h)
   void add_block(const std::string& pre, bool skip) {
-    add(pre + ".norm1.weight", PDM_F32, D);
-    add(pre + ".norm1.bias", PDM_F32, D);
     add(pre + ".attn.qkv.weight", PDM_BF16, 3LL * D * D);
-    if (cfg.qkv_bias) add(pre + ".attn.qkv.bias", PDM_F32, 3LL * D);
+    add(pre + ".attn.qkv.ln_colsum", PDM_F32, 3LL * D);
+    add(pre + ".attn.qkv.ln_bias", PDM_F32, 3LL * D);
     add(pre + ".attn.proj.weight", PDM_BF16, 1LL * D * D);
     add(pre + ".attn.proj.bias", PDM_F32, D);
-    add(pre + ".norm2.weight", PDM_F32, D);
-    add(pre + ".norm2.bias", PDM_F32, D);
     add(pre + ".mlp.fc1.weight", PDM_BF16, 1LL * Hid * D);
-    add(pre + ".mlp.fc1.bias", PDM_F32, Hid);
+    add(pre + ".mlp.fc1.ln_colsum", PDM_F32, Hid);
+    add(pre + ".mlp.fc1.ln_bias", PDM_F32, Hid);
     add(pre + ".mlp.fc2.weight", PDM_BF16, 1LL * D * Hid);
     add(pre + ".mlp.fc2.bias", PDM_F32, D);
     if (skip) {
@@ -103,8 +104,10 @@ namespace {
 // workspace layout
 struct Workspace {
   float* X;     // [rows*Lx, D] residual stream (image)
-  bf16* XB;     // [rows*Lx, D] bf16 copy of x for the next skip_linear
-  bf16* HN;     // [rows*Lmax, D] LayerNorm output
+  bf16* XB;     // [rows*Lx, D] bf16 copy of x (qkv / skip_linear A operand)
+  bf16* XT;     // [rows*Lmax, D] bf16 copy of the block-internal x (after skip_linear / attention)
+  float* ST;    // [rows*Lmax, T] (sum, M2) LayerNorm partials of x at block entry / exit, T = ceil(D/256)
+  float* STT;   // [rows*Lmax, T] partials of the block-internal x
   bf16* QKV;    // [rows*Lmax, 3D]
   bf16* ATT;    // [rows*Lmax, D]
   bf16* MLP;    // [rows*Lmax, Hid]
@@ -115,8 +118,9 @@ struct Workspace {
   bf16* CTXB;   // [rows*n_ctx, clip_dim] bf16 context
   float* MX;    // [rows*Lm, D] mask stream
   bf16* MXB;    // [rows*Lm, D] bf16 copy of the mask-stream block output
-  bf16* MXIN;   // [rows*Lm, D] bf16 copy of the mask-stream block input (skip_linear operand)
+  bf16* MXIN;   // [rows*Lm, D] bf16 copy of the mask-stream block input (qkv / skip_linear operand)
   bf16* SKM;    // [nhalf][rows*Lm, D]
+  float* STM;   // [rows*Lm, T] LayerNorm partials of the mask stream
   size_t bytes;
 };
 
@@ -133,9 +137,12 @@ Workspace layout(const pdm_uvit* h, int rows, char* base) {
   const bool mask = h->cfg.t2i && h->cfg.separate && h->cfg.enable_panoptic;
   const size_t Mm = mask ? (size_t)rows * h->Lm : 0;
   const size_t Mmax = Mx > Mm ? Mx : Mm;
+  const size_t T = (D + 255) / 256;
   w.X = (float*)take(Mx * D * 4);
   w.XB = (bf16*)take(Mx * D * 2);
-  w.HN = (bf16*)take(Mmax * D * 2);
+  w.XT = (bf16*)take(Mmax * D * 2);
+  w.ST = (float*)take(Mmax * T * 8);
+  w.STT = (float*)take(Mmax * T * 8);
   w.QKV = (bf16*)take(Mmax * 3 * D * 2);
   w.ATT = (bf16*)take(Mmax * D * 2);
   w.MLP = (bf16*)take(Mmax * h->Hid * 2);
@@ -149,6 +156,7 @@ Workspace layout(const pdm_uvit* h, int rows, char* base) {
     w.MX = (float*)take(Mm * D * 4);
     w.MXB = (bf16*)take(Mm * D * 2);
     w.MXIN = (bf16*)take(Mm * D * 2);
+    w.STM = (float*)take(Mm * T * 8);
     w.SKM = (bf16*)take((size_t)h->nhalf * Mm * D * 2);
   }
   w.bytes = off;
@@ -161,10 +169,20 @@ struct Ctx {
   hipStream_t s;
 };
 
+// fused-LayerNorm operands of one GEMM: partials produced (st_out) or consumed (st_in + colsum)
+struct LnIO {
+  float* st_out = nullptr;
+  const float* st_in = nullptr;
+  const float* colsum = nullptr;
+};
+
 int gemm(const Ctx& c, const bf16* A, int lda, const bf16* W, const float* bias, int M, int N, int K, int epi,
          bf16* ob, int ldo, float* of, int ldr, int accumulate, const bf16* A2 = nullptr, int lda2 = 0, int K1 = 0,
-         int a_rpg = 0, int a_gs = 0) {
+         int a_rpg = 0, int a_gs = 0, LnIO ln = LnIO()) {
   pdm::GemmArgs a{};
+  const int T = (c.h->D + 255) / 256;
+  a.stats_out = ln.st_out; a.stats_ld = T;
+  a.ln_stats = ln.st_in; a.ln_ld = T; a.ln_D = K; a.ln_eps = 1e-5f; a.ln_colsum = ln.colsum;
   a.A1 = A; a.lda1 = lda;
   a.A2 = A2; a.lda2 = lda2;
   a.K1 = A2 ? K1 : K;
@@ -187,40 +205,38 @@ int gemm(const Ctx& c, const bf16* A, int lda, const bf16* W, const float* bias,
   return PDM_OK;
 }
 
-int layernorm(const Ctx& c, const float* x, const std::string& pre, bf16* y, int rows, int rpg = 1, int gs = 1,
-              int off = 0) {
-  pdm::LayerNormArgs a{};
-  a.x = x; a.ldx = c.h->D;
-  a.gamma = c.h->f(pre + ".weight"); a.beta = c.h->f(pre + ".bias");
-  a.y = y; a.ldy = c.h->D;
-  a.rows = rows; a.D = c.h->D;
-  a.rows_per_group = rpg; a.group_stride = gs; a.row_offset = off;
-  a.eps = 1e-5f;
-  PDM_CHECK(pdm::layernorm_check(a));
-  PDM_HIP(pdm::layernorm_launch(a, c.s));
-  return PDM_OK;
-}
-
 #define PDM_TRY(x)           \
   do {                       \
     int r_ = (x);            \
     if (r_) return r_;       \
   } while (0)
 
-// One U-ViT Block (libs/uvit.py:115-120) on `rows_L` token rows of width D held in X (fp32).
-//   skip_in:  bf16 [rows_L, D] skip activation (out-blocks), with xin_bf16 the bf16 copy of X
-//   xb_out:   where fc2's epilogue writes the bf16 copy of the block output (or null)
-int run_block(const Ctx& c, const std::string& pre, float* X, int nseq, int L, const bf16* xin_bf16,
-              const bf16* skip_in, bf16* xb_out, const Workspace& w) {
+// One U-ViT Block (libs/uvit.py:115-120) on `rows_L` token rows of width D held in X (fp32), with norm1 /
+// norm2 fused into qkv / fc1 (GemmArgs): on entry xb_in = bf16(X) and st_in = the LayerNorm partials of X;
+// the producing epilogues (skip_linear, proj, fc2) leave bf16(x) and its partials for the next consumer.
+//   skip_in:          bf16 [rows_L, D] long-skip activation (out-blocks)
+//   xb_out / st_out:  where fc2's epilogue writes bf16 of the block output and its partials (either may be null)
+int run_block(const Ctx& c, const std::string& pre, float* X, int nseq, int L, const bf16* xb_in, const float* st_in,
+              const bf16* skip_in, bf16* xb_out, float* st_out, const Workspace& w) {
   const pdm_uvit* h = c.h;
   const int D = h->D, M = nseq * L;
-  if (skip_in) {
-    PDM_TRY(gemm(c, xin_bf16, D, h->w(pre + ".skip_linear.weight"), h->f(pre + ".skip_linear.bias"), M, D, 2 * D,
-                 pdm::EPI_F32, nullptr, 0, X, D, 0, skip_in, D, D));
+  const bf16* xb = xb_in;
+  const float* st = st_in;
+  if (skip_in) {  // x = skip_linear(cat([x, skip], -1)): split-K over the two bf16 operands
+    LnIO io;
+    io.st_out = w.STT;
+    PDM_TRY(gemm(c, xb_in, D, h->w(pre + ".skip_linear.weight"), h->f(pre + ".skip_linear.bias"), M, D, 2 * D,
+                 pdm::EPI_F32, w.XT, D, X, D, 0, skip_in, D, D, 0, 0, io));
+    xb = w.XT;
+    st = w.STT;
   }
-  PDM_TRY(layernorm(c, X, pre + ".norm1", w.HN, M));
-  PDM_TRY(gemm(c, w.HN, D, h->w(pre + ".attn.qkv.weight"), h->cfg.qkv_bias ? h->f(pre + ".attn.qkv.bias") : nullptr,
-               M, 3 * D, D, pdm::EPI_BF16, w.QKV, 3 * D, nullptr, 0, 0));
+  {  // qkv = norm1(x) W^T
+    LnIO io;
+    io.st_in = st;
+    io.colsum = h->f(pre + ".attn.qkv.ln_colsum");
+    PDM_TRY(gemm(c, xb, D, h->w(pre + ".attn.qkv.weight"), h->f(pre + ".attn.qkv.ln_bias"), M, 3 * D, D,
+                 pdm::EPI_BF16, w.QKV, 3 * D, nullptr, 0, 0, nullptr, 0, 0, 0, 0, io));
+  }
   {
     pdm::AttentionArgs a{};
     a.qkv = w.QKV; a.ldq = 3 * D;
@@ -230,13 +246,53 @@ int run_block(const Ctx& c, const std::string& pre, float* X, int nseq, int L, c
     PDM_CHECK(pdm::attention_check(a));
     PDM_HIP(pdm::attention_launch(a, c.s));
   }
-  PDM_TRY(gemm(c, w.ATT, D, h->w(pre + ".attn.proj.weight"), h->f(pre + ".attn.proj.bias"), M, D, D, pdm::EPI_F32,
-               nullptr, 0, X, D, 1));
-  PDM_TRY(layernorm(c, X, pre + ".norm2", w.HN, M));
-  PDM_TRY(gemm(c, w.HN, D, h->w(pre + ".mlp.fc1.weight"), h->f(pre + ".mlp.fc1.bias"), M, h->Hid, D, pdm::EPI_GELU,
-               w.MLP, h->Hid, nullptr, 0, 0));
-  PDM_TRY(gemm(c, w.MLP, h->Hid, h->w(pre + ".mlp.fc2.weight"), h->f(pre + ".mlp.fc2.bias"), M, D, h->Hid,
-               pdm::EPI_F32, xb_out, D, X, D, 1));
+  {  // x += proj(attn)
+    LnIO io;
+    io.st_out = w.STT;
+    PDM_TRY(gemm(c, w.ATT, D, h->w(pre + ".attn.proj.weight"), h->f(pre + ".attn.proj.bias"), M, D, D, pdm::EPI_F32,
+                 w.XT, D, X, D, 1, nullptr, 0, 0, 0, 0, io));
+  }
+  {  // h = GELU(fc1(norm2(x)))
+    LnIO io;
+    io.st_in = w.STT;
+    io.colsum = h->f(pre + ".mlp.fc1.ln_colsum");
+    PDM_TRY(gemm(c, w.XT, D, h->w(pre + ".mlp.fc1.weight"), h->f(pre + ".mlp.fc1.ln_bias"), M, h->Hid, D,
+                 pdm::EPI_GELU, w.MLP, h->Hid, nullptr, 0, 0, nullptr, 0, 0, 0, 0, io));
+  }
+  {  // x += fc2(h)
+    LnIO io;
+    io.st_out = st_out;
+    PDM_TRY(gemm(c, w.MLP, h->Hid, h->w(pre + ".mlp.fc2.weight"), h->f(pre + ".mlp.fc2.bias"), M, D, h->Hid,
+                 pdm::EPI_F32, xb_out, D, X, D, 1, nullptr, 0, 0, 0, 0, io));
+  }
+  return PDM_OK;
+}
+
+// bf16 copy + LayerNorm partials of fp32 rows no GEMM epilogue produced (token assembly, mask-stream refresh)
+int row_stats(const Ctx& c, const float* X, int rows, bf16* xb, float* st) {
+  const int D = c.h->D;
+  PDM_HIP(pdm::rowstats_launch(X, D, rows, D, xb, D, st, (D + 255) / 256, c.s));
+  return PDM_OK;
+}
+
+// The single-stream block stack (libs/uvit.py:213-222, libs/uvit_t2i.py:407-410 / 516): X holds the assembled
+// tokens; in-block i leaves bf16 of its output in SK[i] (the long-skip operand and the next block's A operand).
+int run_stack(const Ctx& c, const Workspace& w, int rows, int L) {
+  const pdm_uvit* h = c.h;
+  const size_t MD = (size_t)rows * L * h->D;
+  PDM_TRY(row_stats(c, w.X, rows * L, w.XB, w.ST));
+  const bf16* xb = w.XB;
+  for (int i = 0; i < h->nhalf; ++i) {
+    PDM_TRY(run_block(c, "in_blocks." + std::to_string(i), w.X, rows, L, xb, w.ST, nullptr, w.SK + i * MD, w.ST, w));
+    xb = w.SK + i * MD;
+  }
+  PDM_TRY(run_block(c, "mid_block", w.X, rows, L, xb, w.ST, nullptr, w.XB, w.ST, w));
+  for (int i = 0; i < h->nhalf; ++i) {
+    const bf16* sk = h->cfg.skip ? w.SK + (h->nhalf - 1 - i) * MD : nullptr;
+    const bool last = i + 1 == h->nhalf;
+    PDM_TRY(run_block(c, "out_blocks." + std::to_string(i), w.X, rows, L, w.XB, w.ST, sk, last ? nullptr : w.XB,
+                      last ? nullptr : w.ST, w));
+  }
   return PDM_OK;
 }
 
@@ -484,14 +540,7 @@ int pdm_uvit_forward(pdm_uvit* h, const float* x, const float* t, const int64_t*
     PDM_CHECK(pdm::assemble_check(a));
     PDM_HIP(pdm::assemble_launch(a, c.s));
   }
-  const size_t MD = (size_t)rows * L * D;
-  for (int i = 0; i < h->nhalf; ++i)
-    PDM_TRY(run_block(c, "in_blocks." + std::to_string(i), w.X, rows, L, nullptr, nullptr, w.SK + i * MD, w));
-  PDM_TRY(run_block(c, "mid_block", w.X, rows, L, nullptr, nullptr, w.XB, w));
-  for (int i = 0; i < h->nhalf; ++i) {
-    const bf16* sk = h->cfg.skip ? w.SK + (h->nhalf - 1 - i) * MD : nullptr;
-    PDM_TRY(run_block(c, "out_blocks." + std::to_string(i), w.X, rows, L, w.XB, sk, w.XB, w));
-  }
+  PDM_TRY(run_stack(c, w, rows, L));
   PDM_TRY(final_norm(c, w, rows, w.X, L));
   PDM_TRY(run_head(c, w.HEADIN, h->n_patch, 0, rows, "decoder_pred", h->C, h->P, h->P_pad, eps_pre));
   return PDM_OK;
@@ -528,13 +577,7 @@ int pdm_uvit_t2i_forward(pdm_uvit* h, const float* x, const float* t, const floa
   }
   const size_t MDx = (size_t)rows * Lx * D;
   if (!two) {  // plain text-conditioned U-ViT (mask_token None: 407-410, 516-517)
-    for (int i = 0; i < h->nhalf; ++i)
-      PDM_TRY(run_block(c, "in_blocks." + std::to_string(i), w.X, rows, Lx, nullptr, nullptr, w.SK + i * MDx, w));
-    PDM_TRY(run_block(c, "mid_block", w.X, rows, Lx, nullptr, nullptr, w.XB, w));
-    for (int i = 0; i < h->nhalf; ++i) {
-      const bf16* sk = h->cfg.skip ? w.SK + (h->nhalf - 1 - i) * MDx : nullptr;
-      PDM_TRY(run_block(c, "out_blocks." + std::to_string(i), w.X, rows, Lx, w.XB, sk, w.XB, w));
-    }
+    PDM_TRY(run_stack(c, w, rows, Lx));
     PDM_TRY(final_norm(c, w, rows, w.X, Lx));
     PDM_TRY(run_head(c, w.HEADIN, h->n_patch, 0, rows, "decoder_pred", h->C, h->P, h->P_pad, eps_pre));
     return PDM_OK;
@@ -550,37 +593,43 @@ int pdm_uvit_t2i_forward(pdm_uvit* h, const float* x, const float* t, const floa
     PDM_HIP(pdm::assemble_launch(a, c.s));
   }
   const size_t MDm = (size_t)rows * Lm * D;
-  // mx = cat(x, m): refresh the image half of the mask stream before every mask block (426, 443, 459)
+  // mx = cat(x, m): refresh the image half of the mask stream before every mask block (426, 443, 459), then
+  // the bf16 copy + LayerNorm partials of the whole mask stream (its blocks' qkv / skip_linear operand)
   auto refresh = [&]() -> int {
     PDM_HIP(pdm::rowcopy_launch(w.MX, D, w.X, D, rows * Lx, D, Lx, Lm, Lx, c.s));
-    return PDM_OK;
+    return row_stats(c, w.MX, rows * Lm, w.MXIN, w.STM);
   };
   // x += zeroconv_{2l+1}(mx[:, :Lx]) (435-436, 452-453, 470-472) from the bf16 copy of the mask block output;
-  // the epilogue also leaves the bf16 copy of the new x (the skip / next skip_linear operand) in xb
+  // the epilogue also leaves bf16 of the new x (the skip / next block's operand) in xb and its partials in ST
   auto inject = [&](int layer, const bf16* mxb, bf16* xb) -> int {
     const std::string zc = "zero_convs." + std::to_string(2 * layer + 1) + ".conv";
+    LnIO io;
+    io.st_out = w.ST;
     return gemm(c, mxb, D, h->w(zc + ".weight"), h->f(zc + ".bias"), rows * Lx, D, D, pdm::EPI_F32, xb, D, w.X, D, 1,
-                nullptr, 0, 0, Lx, Lm);
+                nullptr, 0, 0, Lx, Lm, io);
   };
+  PDM_TRY(row_stats(c, w.X, rows * Lx, w.XB, w.ST));
+  const bf16* xb = w.XB;
   int layer = 0;
   for (int i = 0; i < h->nhalf; ++i, ++layer) {
     PDM_TRY(refresh());
-    PDM_TRY(run_block(c, "in_blocks." + std::to_string(i), w.X, rows, Lx, nullptr, nullptr, nullptr, w));
-    PDM_TRY(run_block(c, "in_blocks_mask." + std::to_string(i), w.MX, rows, Lm, nullptr, nullptr, w.SKM + i * MDm, w));
+    PDM_TRY(run_block(c, "in_blocks." + std::to_string(i), w.X, rows, Lx, xb, w.ST, nullptr, nullptr, nullptr, w));
+    PDM_TRY(run_block(c, "in_blocks_mask." + std::to_string(i), w.MX, rows, Lm, w.MXIN, w.STM, nullptr,
+                      w.SKM + i * MDm, nullptr, w));
     PDM_TRY(inject(layer, w.SKM + i * MDm, w.SK + i * MDx));
+    xb = w.SK + i * MDx;
   }
   PDM_TRY(refresh());
-  PDM_TRY(run_block(c, "mid_block", w.X, rows, Lx, nullptr, nullptr, nullptr, w));
-  PDM_TRY(run_block(c, "mid_block_mask", w.MX, rows, Lm, nullptr, nullptr, w.MXB, w));
+  PDM_TRY(run_block(c, "mid_block", w.X, rows, Lx, xb, w.ST, nullptr, nullptr, nullptr, w));
+  PDM_TRY(run_block(c, "mid_block_mask", w.MX, rows, Lm, w.MXIN, w.STM, nullptr, w.MXB, nullptr, w));
   PDM_TRY(inject(layer, w.MXB, w.XB));
   ++layer;
   for (int i = 0; i < h->nhalf; ++i, ++layer) {
     PDM_TRY(refresh());
     const bf16* sk = h->cfg.skip ? w.SK + (h->nhalf - 1 - i) * MDx : nullptr;
-    PDM_TRY(run_block(c, "out_blocks." + std::to_string(i), w.X, rows, Lx, w.XB, sk, nullptr, w));
+    PDM_TRY(run_block(c, "out_blocks." + std::to_string(i), w.X, rows, Lx, w.XB, w.ST, sk, nullptr, nullptr, w));
     const bf16* skm = h->cfg.skip ? w.SKM + (h->nhalf - 1 - i) * MDm : nullptr;
-    if (skm) PDM_HIP(pdm::cast_bf16_launch(w.MX, w.MXIN, (long long)MDm, c.s));
-    PDM_TRY(run_block(c, "out_blocks_mask." + std::to_string(i), w.MX, rows, Lm, w.MXIN, skm, w.MXB, w));
+    PDM_TRY(run_block(c, "out_blocks_mask." + std::to_string(i), w.MX, rows, Lm, w.MXIN, w.STM, skm, w.MXB, nullptr, w));
     PDM_TRY(inject(layer, w.MXB, w.XB));
   }
   // heads (477-519): noise from norm(x) patch tokens; mask head on the un-normalised m (= MX[:, Lx:])
@@ -635,6 +684,29 @@ int pdm_gemm_bf16(const void* A1, int lda1, const void* A2, int lda2, int K1, co
   a.accumulate = accumulate;
   PDM_CHECK(pdm::gemm_check(a, epi));
   PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_gemm_bf16_ln(const void* A, int lda, const void* W, const float* bias, int M, int N, int K, int epi,
+                     void* out_bf16, int ldo, float* out_f32, int ldr, int accumulate, float* stats_out,
+                     const float* ln_stats, const float* ln_colsum, float ln_eps, void* stream) {
+  pdm::GemmArgs a{};
+  a.A1 = (const bf16*)A; a.lda1 = lda; a.K1 = K;
+  a.W = (const bf16*)W; a.bias = bias;
+  a.M = M; a.N = N; a.K = K;
+  a.out_bf16 = (bf16*)out_bf16; a.ldo = ldo;
+  a.out_f32 = out_f32; a.ldr = ldr;
+  a.accumulate = accumulate;
+  a.stats_out = stats_out; a.stats_ld = (N + 255) / 256;
+  a.ln_stats = ln_stats; a.ln_ld = (K + 255) / 256; a.ln_D = K; a.ln_eps = ln_eps; a.ln_colsum = ln_colsum;
+  PDM_CHECK(pdm::gemm_check(a, epi));
+  PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_rowstats(const float* x, int ldx, int rows, int D, void* xb, float* stats, void* stream) {
+  if (!x || !stats || rows <= 0 || D <= 0 || D % 4 || D > 2048) return fail(PDM_ERR_ARG, "pdm_rowstats: bad argument");
+  PDM_HIP(pdm::rowstats_launch(x, ldx, rows, D, (bf16*)xb, D, stats, (D + 255) / 256, (hipStream_t)stream));
   return PDM_OK;
 }
 

@@ -11,6 +11,8 @@
 // with an XOR swizzle (chunk ^ ((row >> 1) & 7)) applied on the SOURCE address, which makes every
 // ds_read_b128 fragment read bank-conflict free.  The MFMA is issued with the weight fragment as the A
 // operand so each lane ends up owning 4 consecutive output columns of one row: 8/16-byte epilogue stores.
+#include <type_traits>
+
 #include "pdm_common.h"
 #include "pdm_kernels.h"
 
@@ -123,17 +125,31 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p, int tiles
   }
 
   // epilogue: lane owns rows m = .. + (lane & 15), columns n .. n+3
+  const bool ln = EPI != EPI_F32 && p.ln_stats != nullptr;
+  float2 mr[4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    mr[mi] = make_float2(0.f, 1.f);
+    if (ln) {
+      const int m = min(m0 + wm * 64 + mi * 16 + (lane & 15), p.M - 1);
+      mr[mi] = ln_merge(p.ln_stats + (size_t)m * p.ln_ld * 2, p.ln_ld, p.ln_D, p.ln_eps);
+    }
+  }
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni) {
     const int n = n0 + wn * 64 + ni * 16 + (lane >> 4) * 4;
     if (n >= p.N) continue;  // N % 4 == 0: a lane's 4 columns are all in or all out
     f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
     if (p.bias) b = *reinterpret_cast<const f32x4*>(p.bias + n);
+    f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (ln) c = *reinterpret_cast<const f32x4*>(p.ln_colsum + n);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       const int m = m0 + wm * 64 + mi * 16 + (lane & 15);
       if (m >= p.M) continue;
-      f32x4 v = acc[ni][mi] + b;
+      f32x4 v = acc[ni][mi];
+      if (ln) v = (v - mr[mi].x * c) * mr[mi].y;
+      v += b;
       if constexpr (EPI == EPI_BF16) {
         *reinterpret_cast<bf16x4*>(p.out_bf16 + (size_t)m * p.ldo + n) = to_bf16x4(v[0], v[1], v[2], v[3]);
       } else if constexpr (EPI == EPI_GELU) {
@@ -160,6 +176,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p, int tiles
 //   BK = 32, NS = 4: 32 KiB slots, 3 in flight, 64-byte rows (half cache lines per load)
 //   BK = 64, NS = 2: 64 KiB slots, 1 in flight, 128-byte rows (full lines)
 constexpr int BM2 = 256, BN2 = 256;
+constexpr int EPI_LDS = 128 * 1024;             // the 256-tile epilogue's staging area; LN row stats follow it
+constexpr int EPI_LDS_EXTRA = 256 * 8;
 
 template <int BK>
 __device__ __forceinline__ int swz_off(int row, int chunk) {
@@ -216,20 +234,47 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
     }
   }
   const bool full = (m0 + 256 <= p.M) && (n0 + 256 <= p.N);
+  // fused LayerNorm consumer: per-row (mean, rstd) of the tile's 256 rows into LDS past the 128 KiB staging
+  // area, per-column sums of the gamma-scaled weight like the bias
+  float2* lnrow = reinterpret_cast<float2*>(smem + EPI_LDS);
+  f32x4 cs[4];
+  const bool ln = EPI != EPI_F32 && p.ln_stats != nullptr;
+  if (ln) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      int ml, nl;
+      frag_pos<MAP>(MAP == 0 ? g * 8 : (g >> 1) * 8 + (g & 1) * 4, lane, wm, wn, ml, nl);
+      cs[g] = *reinterpret_cast<const f32x4*>(p.ln_colsum + min(n0 + nl, p.N - 4));
+    }
+    if (tid < 256) {
+      const int m = min(m0 + tid, p.M - 1);
+      lnrow[tid] = ln_merge(p.ln_stats + (size_t)m * p.ln_ld * 2, p.ln_ld, p.ln_D, p.ln_eps);
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
+    auto stage = [&](auto with_ln) {
 #pragma unroll
-    for (int f = 0; f < 32; ++f) {
-      int ml, nl;
-      frag_pos<MAP>(f, lane, wm, wn, ml, nl);
-      f32x4 v = acc[f] + bv[MAP == 0 ? f / 8 : (f / 8 & 1) * 2 + (f / 4 & 1)];
-      if constexpr (EPI == EPI_GELU) {
-        v[0] = gelu_erf(v[0]); v[1] = gelu_erf(v[1]); v[2] = gelu_erf(v[2]); v[3] = gelu_erf(v[3]);
+      for (int f = 0; f < 32; ++f) {
+        int ml, nl;
+        frag_pos<MAP>(f, lane, wm, wn, ml, nl);
+        const int gi = MAP == 0 ? f / 8 : (f / 8 & 1) * 2 + (f / 4 & 1);
+        f32x4 v = acc[f];
+        if constexpr (decltype(with_ln)::value) {
+          const float2 mr = lnrow[ml];
+          v = (v - mr.x * cs[gi]) * mr.y;
+        }
+        v += bv[gi];
+        if constexpr (EPI == EPI_GELU) {
+          v[0] = gelu_erf(v[0]); v[1] = gelu_erf(v[1]); v[2] = gelu_erf(v[2]); v[3] = gelu_erf(v[3]);
+        }
+        const int off = ml * 512 + ((((nl >> 3) ^ (ml & 31)) << 4) | ((nl & 4) << 1));
+        *reinterpret_cast<bf16x4*>(smem + off) = to_bf16x4(v[0], v[1], v[2], v[3]);
       }
-      const int off = ml * 512 + ((((nl >> 3) ^ (ml & 31)) << 4) | ((nl & 4) << 1));
-      *reinterpret_cast<bf16x4*>(smem + off) = to_bf16x4(v[0], v[1], v[2], v[3]);
-    }
+    };
+    if (ln) stage(std::true_type{});
+    else stage(std::false_type{});
     __syncthreads();
     i32x4 v[16];
 #pragma unroll
@@ -254,7 +299,32 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
     }
     return;
   }
-  // fp32: the thread's 8 store columns n0 + (tid & 31) * 8 are the same in every row it stores
+  // fp32: the thread's 8 store columns n0 + (tid & 31) * 8 are the same in every row it stores; the 32
+  // threads of a half-wave hold one whole 256-column row, so the LayerNorm partials of the row are two
+  // half-wave reductions (sum, then M2 about the group mean)
+  const int ncols = min(256, p.N - n0);
+  auto row_stats = [&](const f32x4& a, const f32x4& b, int m, int n) {
+    float sv = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sv += n + j < p.N ? a[j] : 0.f;
+      sv += n + 4 + j < p.N ? b[j] : 0.f;
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) sv += __shfl_xor(sv, o, 64);
+    const float mu = sv / (float)ncols;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d0 = a[j] - mu, d1 = b[j] - mu;
+      q += n + j < p.N ? d0 * d0 : 0.f;
+      q += n + 4 + j < p.N ? d1 * d1 : 0.f;
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    if ((tid & 31) == 0 && m < p.M)
+      *reinterpret_cast<float2*>(p.stats_out + ((size_t)m * p.stats_ld + (n0 >> 8)) * 2) = make_float2(sv, q);
+  };
   f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
   if (p.bias) {
     const int n = min(n0 + (tid & 31) * 8, p.N - 8 >= 0 ? p.N - 8 : 0);
@@ -310,6 +380,13 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
             *reinterpret_cast<bf16x8*>(p.out_bf16 + m * p.ldo + n) = o;
           }
         }
+        if (p.stats_out) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int idx = (g * 4 + i) * 512 + tid;
+            row_stats(v0[i], v1[i], m0 + pass * 128 + (idx >> 5), n0 + (idx & 31) * 8);
+          }
+        }
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -330,7 +407,10 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
               for (int j = 0; j < 4; ++j) { o[j] = (bf16)a[j]; o[4 + j] = (bf16)b[j]; }
               *reinterpret_cast<bf16x8*>(p.out_bf16 + (size_t)m * p.ldo + n) = o;
             }
+            v0[i] = a;
+            v1[i] = b;
           }
+          if (p.stats_out) row_stats(v0[i], v1[i], m, n);
         }
       }
     }
@@ -915,6 +995,14 @@ const char* gemm_check(const GemmArgs& p, int epi) {
     if (p.conv_up && (p.convH % 2 || p.convW % 2)) return "gemm(conv): upsampled grid must be even";
   }
   if (((uintptr_t)p.A1 | (uintptr_t)p.W | (uintptr_t)(p.A2 ? p.A2 : p.A1)) & 15) return "gemm: operands must be 16-byte aligned";
+  if (p.stats_out && (epi != EPI_F32 || p.stats_ld < (p.N + 255) / 256 || ((uintptr_t)p.stats_out & 7)))
+    return "gemm: LayerNorm stats need the fp32 epilogue and stats_ld >= ceil(N / 256)";
+  if ((p.stats_out || p.ln_stats) && p.batch > 1) return "gemm: fused LayerNorm is not available for batched GEMMs";
+  if (p.ln_stats) {
+    if (epi == EPI_F32) return "gemm: the fused LayerNorm applies to the bf16 / GELU epilogues";
+    if (!p.ln_colsum || ((uintptr_t)p.ln_colsum & 15) || p.ln_D <= 0 || p.ln_ld != (p.ln_D + 255) / 256)
+      return "gemm: fused LayerNorm needs ln_colsum and ln_ld = ceil(ln_D / 256)";
+  }
   if (epi == EPI_BF16 || epi == EPI_GELU) {
     if (!p.out_bf16 || (p.ldo % 4)) return "gemm: bf16 output missing or ldo not a multiple of 4";
   } else if (epi == EPI_F32) {
@@ -931,7 +1019,7 @@ void gemm_set_algo(int algo) { g_gemm_algo = algo; }
 
 template <int BK, int NS>
 static hipError_t launch256(const GemmArgs& p, int epi, hipStream_t stream) {
-  constexpr int SMEM = (BM2 + BN2) * BK * 2 * NS;
+  constexpr int SMEM = (BM2 + BN2) * BK * 2 * NS + EPI_LDS_EXTRA;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI_BF16, BK, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
@@ -952,7 +1040,7 @@ static hipError_t launch256(const GemmArgs& p, int epi, hipStream_t stream) {
 
 template <int CONV>
 static hipError_t launch8p(const GemmArgs& p, int epi, hipStream_t stream) {
-  constexpr int SMEM = 2 * 4 * 128 * 128;   // 128 KiB
+  constexpr int SMEM = 2 * 4 * 128 * 128 + EPI_LDS_EXTRA;   // 128 KiB ring + LN row stats
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI_BF16, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
@@ -973,7 +1061,7 @@ static hipError_t launch8p(const GemmArgs& p, int epi, hipStream_t stream) {
 
 template <int CONV, int SCHED>
 static hipError_t launch8d(const GemmArgs& p, int epi, hipStream_t stream) {
-  constexpr int SMEM = 2 * 4 * 128 * 128;   // 128 KiB
+  constexpr int SMEM = 2 * 4 * 128 * 128 + EPI_LDS_EXTRA;   // 128 KiB ring + LN row stats
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm8d_kernel<EPI_BF16, CONV, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
@@ -1030,7 +1118,11 @@ hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream) {
     case EPI_GELU: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_GELU>, grid, block, SMEM_BYTES, stream, p, tiles_n, nwg); break;
     default: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_F32>, grid, block, SMEM_BYTES, stream, p, tiles_n, nwg); break;
   }
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  // the 128-tile epilogue spreads a row over two waves: its LayerNorm partials come from a row pass instead
+  if (e == hipSuccess && p.stats_out && p.batch <= 1)
+    e = rowstats_launch(p.out_f32, p.ldr, p.M, p.N, nullptr, 0, p.stats_out, p.stats_ld, stream);
+  return e;
 }
 
 }  // namespace pdm

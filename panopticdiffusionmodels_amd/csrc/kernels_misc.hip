@@ -61,6 +61,32 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs p) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// LayerNorm row partials for the fused LayerNorm (see GemmArgs): one wave per row; float4 chunk i of the row
+// covers columns 256 i .. 256 i + 255, i.e. exactly one partial group, so each group is two wave sums.
+template <int NV>
+__global__ __launch_bounds__(256) void rowstats_kernel(const float* x, int ldx, int rows, int D, bf16* xb, int ldb,
+                                                       float* stats, int stats_ld) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const f32x4* xr = reinterpret_cast<const f32x4*>(x + (size_t)r * ldx);
+  const int nv = D >> 2;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int idx = lane + i * 64;
+    if (i * 64 >= nv) break;
+    const bool ok = idx < nv;
+    const f32x4 v = ok ? xr[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (ok && xb) *reinterpret_cast<bf16x4*>(xb + (size_t)r * ldb + 4 * idx) = to_bf16x4(v[0], v[1], v[2], v[3]);
+    const float s = wave_sum((v[0] + v[1]) + (v[2] + v[3]));
+    const float mu = s / (float)min(256, D - 256 * i);
+    const f32x4 d = v - mu;
+    const float q = wave_sum(ok ? (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]) : 0.f);
+    if (lane == 0) *reinterpret_cast<float2*>(stats + ((size_t)r * stats_ld + i) * 2) = make_float2(s, q);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Token assembly (libs/uvit.py:201-212; libs/uvit_t2i.py:382-409): block (x = 0) writes the extra
 // tokens of one sample, blocks x >= 1 write 16 patch tokens each: PatchEmbed conv (k = s = p, K order
 // (C, p1, p2): libs/uvit.py:129) + bias + pos_embed, fp32.
@@ -324,6 +350,16 @@ hipError_t layernorm_launch(const LayerNormArgs& p, hipStream_t stream) {
     case 6: hipLaunchKernelGGL(layernorm_kernel<6>, grid, block, 0, stream, p); break;
     default: hipLaunchKernelGGL(layernorm_kernel<8>, grid, block, 0, stream, p); break;
   }
+  return hipGetLastError();
+}
+
+hipError_t rowstats_launch(const float* x, int ldx, int rows, int D, bf16* xb, int ldb, float* stats, int stats_ld,
+                           hipStream_t stream) {
+  if (!x || !stats || rows <= 0 || D <= 0 || D % 4 || D > 2048 || stats_ld < (D + 255) / 256 || ldx % 4 ||
+      (xb && ldb % 4))
+    return hipErrorInvalidValue;
+  dim3 grid((rows + 3) / 4), block(256);
+  hipLaunchKernelGGL(rowstats_kernel<8>, grid, block, 0, stream, x, ldx, rows, D, xb, ldb, stats, stats_ld);
   return hipGetLastError();
 }
 

@@ -54,6 +54,21 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Fused LayerNorm: merge one row's ceil(D/256) partials (sum, M2 about the group mean; groups of 256 columns,
+// the last one D - 256 t wide) with Chan's update -> (mean, 1/sqrt(var + eps)), biased variance like torch.
+__device__ __forceinline__ float2 ln_merge(const float* st, int T, int D, float eps) {
+  float sum = 0.f;
+  for (int t = 0; t < T; ++t) sum += st[2 * t];
+  const float mean = sum / (float)D;
+  float m2 = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float n = (float)min(256, D - 256 * t);
+    const float d = st[2 * t] / n - mean;
+    m2 += st[2 * t + 1] + n * d * d;
+  }
+  return make_float2(mean, 1.0f / sqrtf(m2 / (float)D + eps));
+}
+
 __device__ __forceinline__ bf16x4 to_bf16x4(float a, float b, float c, float d) {
   bf16x4 r;
   r[0] = (bf16)a; r[1] = (bf16)b; r[2] = (bf16)c; r[3] = (bf16)d;

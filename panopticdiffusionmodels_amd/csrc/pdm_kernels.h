@@ -31,7 +31,21 @@ struct GemmArgs {
   // (b, y, x) of an convH x convW grid, K = 9 * convC in (ky, kx, ci) order, padded taps read `zero`.
   int conv, convH, convW, convC, conv_up;   // conv_up: source is the nearest-x2 upsample (Hs = H/2)
   const bf16* zero;           // >= 256 zero bytes
+  // LayerNorm fusion (norm1 -> qkv, norm2 -> fc1: libs/uvit.py:100,103,115-120), see ln_partials below.
+  //  producer (EPI_F32 with stats_out): per stored row m and 256-column group t = n / 256 writes the group's
+  //    (sum, M2 about the group mean) of the final fp32 values to stats_out[(m * stats_ld + t) * 2 + {0,1}]
+  //  consumer (EPI_BF16 / EPI_GELU with ln_stats): A holds bf16(x) un-normalised, W = W_ref * diag(gamma),
+  //    out[m, n] = rstd_m * (acc - mean_m * ln_colsum[n]) + bias[n]   (bias = W_ref beta (+ b_ref))
+  //    with mean_m / rstd_m merged from the ln_D-column row's partials (Chan), eps ln_eps
+  float* stats_out; int stats_ld;
+  const float* ln_stats; int ln_ld; int ln_D; float ln_eps; const float* ln_colsum;
 };
+
+// Row partials of the fused LayerNorm: X fp32 [rows, D] -> stats [rows, ceil(D/256)] (sum, M2) per 256-column
+// group (+ optional bf16 copy xb [rows, D]).  Used where no GEMM epilogue produced them (token assembly, the
+// t2i mask-stream refresh, and behind the 128-tile GEMM policy).
+hipError_t rowstats_launch(const float* x, int ldx, int rows, int D, bf16* xb, int ldb, float* stats, int stats_ld,
+                           hipStream_t stream);
 
 const char* gemm_check(const GemmArgs& p, int epi);
 hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream);

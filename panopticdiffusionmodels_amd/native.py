@@ -3,8 +3,8 @@
 The module keeps fp32 parameters under the reference's state_dict keys (so `load_state_dict` of a
 reference checkpoint works unchanged, eval_ldm_discrete.py:46).  On first GPU use the parameters are
 packed once into the layouts libpdm expects (Linear weights -> bf16 [out, in]; decoder heads padded to a
-multiple of 16 rows; conv / embedding tables fp32) and their device addresses are registered with the
-handle.  Any load_state_dict / .to() invalidates the packed copy.
+multiple of 16 rows; conv / embedding tables fp32; norm1 / norm2 folded into attn.qkv / mlp.fc1, see
+`_ln_fold`) and their device addresses are registered with the handle.  Any load_state_dict / .to() invalidates the packed copy.
 """
 import ctypes
 
@@ -66,7 +66,37 @@ class NativeHandle:
         _lib.check(lib.pdm_uvit_validate(h), "pdm_uvit_validate")
 
     @staticmethod
+    def _ln_fold(sd, name):
+        """norm1 -> attn.qkv and norm2 -> mlp.fc1 are fused (libs/uvit.py:115-120): LN(x) W^T + b =
+        rstd * (x (W diag(g))^T - mean * colsum) + (W beta + b).  Returns the packed tensor for the folded
+        weight / its row sums / the folded bias, or None when `name` is not one of them."""
+        for lin, norm in ((".attn.qkv", ".norm1"), (".mlp.fc1", ".norm2")):
+            for part in (".weight", ".ln_colsum", ".ln_bias"):
+                if not name.endswith(lin + part):
+                    continue
+                pre = name[: -len(lin + part)]
+                w = sd[pre + lin + ".weight"].detach().float()
+                g = sd[pre + norm + ".weight"].detach().float()
+                wg = (w * g[None, :]).to(torch.bfloat16)
+                if part == ".weight":
+                    return wg
+                if part == ".ln_colsum":
+                    return wg.double().sum(1).float()
+                b = (w.double() @ sd[pre + norm + ".bias"].detach().double())
+                if pre + lin + ".bias" in sd:
+                    b = b + sd[pre + lin + ".bias"].detach().double()
+                return b.float()
+        return None
+
+    @staticmethod
     def _pack(sd, name, dtype, numel, dev):
+        folded = NativeHandle._ln_fold(sd, name)
+        if folded is not None:
+            t = folded.to(device=dev, dtype=torch.bfloat16 if dtype == _lib.PDM_BF16 else torch.float32)
+            t = t.contiguous().reshape(-1)
+            if t.numel() != numel:
+                raise RuntimeError(f"parameter {name!r}: {t.numel()} elements, the HIP layout expects {numel}")
+            return t
         if name not in sd:
             raise RuntimeError(f"parameter {name!r} missing from the module state_dict")
         src = sd[name].detach()

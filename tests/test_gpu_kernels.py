@@ -141,6 +141,74 @@ def test_gemm_batched(lib, algo, Z, M, N, K):
         lib.load().pdm_set_gemm_algo(0)
 
 
+def _ref_partials(y):
+    """(sum, M2 about the group mean) per 256-column group of fp32 rows y, float64."""
+    y = y.double()
+    out = []
+    for t in range(0, y.shape[1], 256):
+        g = y[:, t:t + 256]
+        out.append(torch.stack([g.sum(1), ((g - g.mean(1, keepdim=True)) ** 2).sum(1)], 1))
+    return torch.stack(out, 1)
+
+
+@pytest.mark.parametrize("rows,D", [(1, 64), (517, 1024), (300, 1152), (33, 512), (7, 576)])
+def test_rowstats(lib, rows, D):
+    g = torch.Generator(device="cuda").manual_seed(rows + D)
+    x = torch.randn(rows, D, device="cuda", generator=g) * 3 + 1
+    xb, st = lib.rowstats(x)
+    assert torch.equal(xb, x.bfloat16())
+    ref = _ref_partials(x)
+    assert rel(st, ref) < 1e-5
+
+
+@pytest.mark.parametrize("algo", [1, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("M,N,K,epi", [(4133, 1024, 1024, "bf16"), (515, 4096, 1024, "gelu"), (9000, 3456, 1152, "bf16"),
+                                       (700, 520, 512, "gelu")])
+def test_gemm_layernorm_consumer(lib, algo, M, N, K, epi):
+    """norm -> Linear fused (libs/uvit.py:100,103): bf16(x) operand, gamma-scaled weight, per-row mean / rstd
+    merged from the 256-column partials, vs F.layer_norm + linear in fp32.  The mean is large on purpose (|mean|
+    ~ 2 std) so the mean-correction term is exercised."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + algo)
+    x = torch.randn(M, K, device="cuda", generator=g) * 1.5 + 3.0 * torch.randn(M, 1, device="cuda", generator=g)
+    gamma = 1.0 + 0.3 * torch.randn(K, device="cuda", generator=g)
+    beta = 0.2 * torch.randn(K, device="cuda", generator=g)
+    w = torch.randn(N, K, device="cuda", generator=g) * K ** -0.5
+    b = 0.1 * torch.randn(N, device="cuda", generator=g)
+    ref = F.layer_norm(x, (K,), gamma, beta, eps=1e-5) @ w.t() + b
+    if epi == "gelu":
+        ref = F.gelu(ref)
+    wg = (w * gamma[None]).bfloat16()
+    colsum = wg.double().sum(1).float()
+    bias = (w.double() @ beta.double() + b.double()).float()
+    xb, st = lib.rowstats(x)
+    lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
+    try:
+        out = lib.gemm_ln(xb, wg, bias, lib.EPI_GELU if epi == "gelu" else lib.EPI_BF16, ln_stats=st, ln_colsum=colsum)
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+    assert rel(out.float(), ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("algo", [1, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("M,N,K", [(4133, 1024, 1024), (515, 1152, 2048), (8192, 512, 256)])
+def test_gemm_layernorm_producer(lib, algo, M, N, K):
+    """Residual epilogue emitting the LayerNorm partials of the stored fp32 rows (+ the bf16 copy)."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + algo + 1)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    r0 = torch.randn(M, N, device="cuda", generator=g) + 2.0
+    cp = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
+    try:
+        out, st = lib.gemm_ln(a, w, bias, lib.EPI_F32, out=cp, out_f32=r0.clone(), accumulate=True, stats_out=True)
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+    assert rel(out, a.float() @ w.float().t() + bias + r0) < 2e-3
+    assert torch.equal(cp, out.bfloat16())
+    assert rel(st, _ref_partials(out)) < 1e-5
+
+
 def test_gemm_bad_shape(lib):
     a = torch.zeros(16, 100, device="cuda", dtype=torch.bfloat16)
     w = torch.zeros(128, 100, device="cuda", dtype=torch.bfloat16)
