@@ -47,6 +47,7 @@ _SIGS = {
     "pdm_device_arch": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     "pdm_set_gemm_algo": (ctypes.c_int, [ctypes.c_int]),
     "pdm_set_attention_algo": (ctypes.c_int, [ctypes.c_int]),
+    "pdm_set_gemm_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "pdm_uvit_create": (ctypes.c_int, [ctypes.POINTER(PdmUvitCfg), ctypes.POINTER(ctypes.c_void_p)]),
     "pdm_uvit_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "pdm_uvit_set_param": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int,

@@ -351,6 +351,12 @@ int pdm_set_gemm_algo(int algo) {
   return PDM_OK;
 }
 
+int pdm_set_gemm_tuning(int raster, int dbg_tile0) {
+  if (raster < 0 || raster > 64) return fail(PDM_ERR_ARG, "pdm_set_gemm_tuning: raster must be in [0, 64]");
+  pdm::gemm_set_tuning(raster, dbg_tile0);
+  return PDM_OK;
+}
+
 int pdm_set_attention_algo(int algo) {
   if (algo < 0 || algo > 3) return fail(PDM_ERR_ARG, "pdm_set_attention_algo: algo must be 0 (auto), 1, 2 or 3");
   pdm::attention_set_algo(algo);

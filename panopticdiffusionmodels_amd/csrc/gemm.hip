@@ -745,8 +745,20 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
     const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
   }
-  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
+  int tm, tn;
+  if (p.raster > 0) {   // groups of `raster` row panels, column-major inside a group (L2 reuse of A and W)
+    const int tiles_m = (p.M + BM2 - 1) / BM2;
+    const int grp = bid / (p.raster * tiles_n);
+    const int rows_in = min(p.raster, tiles_m - grp * p.raster);
+    const int r = bid - grp * p.raster * tiles_n;
+    tm = grp * p.raster + r % rows_in;
+    tn = r / rows_in;
+  } else {
+    tm = bid / tiles_n;
+    tn = bid - tm * tiles_n;
+  }
   const int m0 = tm * BM2, n0 = tn * BN2;
+  const int lm0 = p.dbg_tile0 ? 0 : m0, ln0 = p.dbg_tile0 ? 0 : n0;   // operand origin of the staging loads
   if (p.batch > 1) {
     const long long z = blockIdx.y;
     p.A1 += z * p.sA;
@@ -776,7 +788,7 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
     const unsigned sb = (unsigned)((pch ^ ((row >> 1) & 7)) * 16);   // logical chunk stored at physical pch
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int gm = m0 + h * 128 + row;
+      const int gm = lm0 + h * 128 + row;
       if constexpr (CONV) {
         if (gm < p.M) {
           const int hw = p.convH * p.convW, b = gm / hw, r = gm - b * hw, y = r / p.convW;
@@ -792,7 +804,7 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
         a2off[h][i] = gm < p.M ? (unsigned)gm * (unsigned)(p.lda2 * 2) + sb : OOB;
         cpix[h][i] = 0;
       }
-      const int gn = n0 + h * 128 + row;
+      const int gn = ln0 + h * 128 + row;
       woff[h][i] = gn < p.N ? (unsigned)gn * (unsigned)(ldw * 2) + sb : OOB;
     }
   }
@@ -1014,7 +1026,9 @@ const char* gemm_check(const GemmArgs& p, int epi) {
   return nullptr;
 }
 
-static int g_gemm_algo = 0;  // 0 auto, 1 = 128x128, 2 = 256x256 BK32 x4 ring, 3 = 256x256 BK64 x2, 4 = 256x256 8-phase
+static int g_gemm_algo = 0;
+static int g_gemm_raster = 0, g_gemm_dbg = 0;
+void gemm_set_tuning(int raster, int dbg_tile0) { g_gemm_raster = raster; g_gemm_dbg = dbg_tile0; }  // 0 auto, 1 = 128x128, 2 = 256x256 BK32 x4 ring, 3 = 256x256 BK64 x2, 4 = 256x256 8-phase
 void gemm_set_algo(int algo) { g_gemm_algo = algo; }
 
 template <int BK, int NS>
@@ -1093,9 +1107,14 @@ static bool fits_rsrc(const GemmArgs& p) {
   return a1 < lim && a2 < lim && w < lim && (!p.conv || p.convW < 4096);
 }
 
-hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream) {
+hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
+  GemmArgs p = args;
+  // tile order: groups of 8 row panels once there are >= 8 column tiles (an XCD's 32 resident tiles then share
+  // 4 A and 8 W panels instead of 2 and 16); measured by tools/gemm_tune.py
+  p.raster = g_gemm_raster ? g_gemm_raster : (p.N >= 8 * BN2 ? 8 : 0);
+  p.dbg_tile0 = g_gemm_dbg;
   int algo = g_gemm_algo;
-  if (algo == 0) algo = (p.M >= 4096 && p.N >= 256) ? 3 : 1;
+  if (algo == 0) algo = (p.M >= 4096 && p.N >= 256) ? 7 : 1;
   // the 256-tile bf16 epilogue stores 16-byte row chunks: needs N, ldo multiples of 8 and an aligned output
   if ((epi == EPI_BF16 || epi == EPI_GELU) && (p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))) algo = 1;
   if (epi == EPI_F32 && (p.N % 8 || p.ldr % 4 || ((uintptr_t)p.out_f32 & 15) ||

@@ -39,7 +39,11 @@ struct GemmArgs {
   //    with mean_m / rstd_m merged from the ln_D-column row's partials (Chan), eps ln_eps
   float* stats_out; int stats_ld;
   const float* ln_stats; int ln_ld; int ln_D; float ln_eps; const float* ln_colsum;
+  // tuning knobs (set by gemm_launch): raster = row panels per tile group inside an XCD's range (0: row-major);
+  // dbg_tile0 = stage every tile's operands from tile (0, 0) (timing experiments only: wrong results)
+  int raster, dbg_tile0;
 };
+void gemm_set_tuning(int raster, int dbg_tile0);
 
 // Row partials of the fused LayerNorm: X fp32 [rows, D] -> stats [rows, ceil(D/256)] (sum, M2) per 256-column
 // group (+ optional bf16 copy xb [rows, D]).  Used where no GEMM epilogue produced them (token assembly, the
