@@ -11,6 +11,8 @@
 // and P^T feeds the P V MFMA as its B operand with no lane movement (the k order inside a 32-key step is
 // permuted consistently on both operands).  V^T fragments come from ds_read_b64_tr_b16 transposed reads of
 // the row-major V chunk.
+#include <type_traits>
+
 #include "pdm_common.h"
 #include "pdm_kernels.h"
 
@@ -354,6 +356,264 @@ __global__ __launch_bounds__(T == 2 ? 768 : 512) void attention_kv_kernel(Attent
     }
   }
 }
+
+// ------------------------------------------------------------------------------------------------
+// Head-resident v2 (Dh = 64): a 4-wave workgroup per (b, h), two workgroups per CU (LDS-bound), so one
+// head's K/V DMA overlaps the other head's math.  K and V (L x 128 B each, layouts as above) are staged by
+// LDS-DMA in 64-key blocks; the first pass waits per block (counted vmcnt + one barrier), so its math starts
+// as soon as block 0 has landed.  Q fragments of a wave's first pass are loaded by inline-asm global loads
+// issued ahead of the DMA and waited for explicitly (a compiler-visible load would drain the DMA queue).
+// Wave w owns query tiles w, w + 4, w + 8, ... and runs them two at a time, so each K and V^T fragment read
+// feeds two MFMAs.  DEBUG 1: loads only; DEBUG 2: math only (timing experiments, wrong results).
+__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
+  switch (n) {
+#define PDM_W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    PDM_W(0) PDM_W(1) PDM_W(2) PDM_W(3) PDM_W(4) PDM_W(5) PDM_W(6) PDM_W(7) PDM_W(8) PDM_W(9) PDM_W(10)
+    PDM_W(11) PDM_W(12) PDM_W(13) PDM_W(14) PDM_W(15) PDM_W(16) PDM_W(17) PDM_W(18) PDM_W(19) PDM_W(20)
+    PDM_W(21) PDM_W(22) PDM_W(23) PDM_W(24) PDM_W(25) PDM_W(26) PDM_W(27) PDM_W(28) PDM_W(29) PDM_W(30)
+#undef PDM_W
+    default: asm volatile("s_waitcnt vmcnt(31)" ::: "memory"); break;
+  }
+}
+
+__device__ __forceinline__ i32x4 gload16_asm(const void* ptr) {
+  i32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
+  return v;
+}
+
+// cross-lane max / sum over the four 16-lane rows holding one query's keys (lanes col, col+16, col+32,
+// col+48): v_permlane16/32_swap half exchanges, no LDS round trip (ds_bpermute)
+__device__ __forceinline__ float xrow_max(float v) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float xrow_sum(float v) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+template <int DEBUG>
+__global__ __launch_bounds__(256, 2) void attention_v2_kernel(AttentionArgs p, int nqt, int Lp) {
+  constexpr int DH = 64;
+  constexpr float RESCALE_THR = 8.0f;   // deferred rescale (log2 units): P <= 2^8 in bf16, O / l stay fp32
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* Ks = lds;
+  char* Vs = lds + Lp * 128;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar waits and branches
+  const int bh = blockIdx.x;
+  const int b = bh / p.H, h = bh % p.H;
+  const int L = p.L, D = p.H * DH;
+  const bf16* base = p.qkv + (size_t)b * L * p.ldq + h * DH;
+  const int g = lane >> 4, col = lane & 15;
+
+  // tiles of this wave: w, w+4, ...; passes of two tiles (the last pass may hold one)
+  const int my_tiles = nqt > wave ? (nqt - wave + 3) / 4 : 0;
+  const int npass = (my_tiles + 1) / 2;
+
+  auto qptr = [&](int tile, int ks) {
+    int q = tile * 16 + col;
+    q = q < L ? q : L - 1;
+    return base + (size_t)q * p.ldq + ks * 32 + g * 8;
+  };
+  // Q fragments of the first pass (B operand): lane holds Q[q = tile*16 + col][d = ks*32 + g*8 .. +8], loaded
+  // by inline asm ahead of the K/V DMA (a compiler-visible load would make hipcc drain the DMA queue)
+  i32x4 q0[2][2];
+  if (npass > 0 && DEBUG != 2) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int tile = min(wave + 4 * t, nqt - 1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) q0[t][ks] = gload16_asm(qptr(tile, ks));
+    }
+  }
+  // K / V DMA in 64-key blocks: block c = row groups 8c .. 8c+7 (8 rows x 128 B each); wave w stages groups
+  // 8c + w and 8c + w + 4 of K and of V, so a block is 4 LDS-DMA per wave (the last block may have fewer)
+  const int ngrp = Lp / 8;
+  if (DEBUG != 2) {
+    const int r8 = lane >> 3, pc = lane & 7;
+    for (int grp0 = 0; grp0 < ngrp; grp0 += 8) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int grp = grp0 + wave + 4 * i;
+        if (grp < ngrp) {
+          const int row = grp * 8 + r8;
+          const int key = row < L ? row : L - 1;
+          const bf16* src = base + (size_t)key * p.ldq;
+          const int kc = pc ^ ((row >> 1) & 7);
+          const int vc = ((((pc >> 1) ^ ((row >> 1) & 3)) << 1) | (pc & 1));
+          glds16(src + D + kc * 8, (PDM_LDS void*)(Ks + grp * 1024));
+          glds16(src + 2 * D + vc * 8, (PDM_LDS void*)(Vs + grp * 1024));
+        }
+      }
+    }
+  }
+  // LDS-DMA ops this wave issued for blocks > c (the vmcnt that retires Q and blocks 0..c)
+  auto ops_after = [&](int c) {
+    int n = 0;
+    for (int grp0 = (c + 1) * 8; grp0 < ngrp; grp0 += 8)
+      for (int i = 0; i < 2; ++i) n += (grp0 + wave + 4 * i < ngrp) ? 2 : 0;
+    return n;
+  };
+  auto block_ready = [&](int c) {   // pass 0: block c of K/V landed (all waves) before anyone reads it
+    if (DEBUG == 0) wait_vmcnt_dyn(ops_after(c));
+    else if (DEBUG == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const float sl2 = p.scale * 1.4426950408889634f;
+  const int nfull = L / 64, nch = (L + 63) / 64;
+
+  // one pass over all keys for NT query tiles (qf), writing the normalised rows of tiles tl[0..NT)
+  auto run_pass = [&](auto ntc, const bf16x8 (&qf)[2][2], const int (&tl)[2], bool first) {
+    constexpr int NT = decltype(ntc)::value;
+    float m_run[NT], l_run[NT];
+    f32x4 acc[NT][4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      m_run[t] = -INFINITY;
+      l_run[t] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto do_block = [&](int c, auto tailc) {
+      constexpr bool TAIL = decltype(tailc)::value;
+      const int kvalid = L - c * 64;
+      f32x4 s[NT][4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (TAIL && kt * 16 >= kvalid) continue;
+        const int row = c * 64 + kt * 16 + col;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + row * 128 + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 4));
+#pragma unroll
+          for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kf, qf[t][ks], s[t][kt]);
+        }
+      }
+      if constexpr (TAIL) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (kt * 16 + g * 4 + j >= kvalid)
+#pragma unroll
+              for (int t = 0; t < NT; ++t) s[t][kt][j] = -INFINITY;
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4 m4 = s[t][0];
+#pragma unroll
+        for (int kt = 1; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) m4[j] = fmaxf(m4[j], s[t][kt][j]);
+        const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]))) * sl2;
+        // deferred rescale: keep the running max until a block exceeds it by RESCALE_THR
+        const bool grow = cmax > m_run[t] + RESCALE_THR;
+        const float m_new = grow ? cmax : m_run[t];
+        const float alpha = __builtin_amdgcn_exp2f(m_run[t] - m_new);
+        m_run[t] = m_new;
+        f32x4 l4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(fmaf(s[t][kt][j], sl2, -m_new));
+          l4 += s[t][kt];
+        }
+        l_run[t] = fmaf(l_run[t], alpha, (l4[0] + l4[1]) + (l4[2] + l4[3]));
+        if (__builtin_amdgcn_ballot_w64(grow)) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[t][i] *= alpha;
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (TAIL && kk * 32 >= kvalid) break;
+        bf16x8 pf[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pf[t][j] = (bf16)s[t][2 * kk][j];
+            pf[t][4 + j] = (bf16)s[t][2 * kk + 1][j];
+          }
+        const int qq = col >> 2, pp = col & 3;
+        const int r1 = c * 64 + kk * 32 + 4 * g + qq, r2 = r1 + 16;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const s16x4 lo = lds_read_tr16(Vs + r1 * 128 + ((dt ^ ((r1 >> 1) & 3)) << 5) + 8 * pp);
+          const s16x4 hi = lds_read_tr16(Vs + r2 * 128 + ((dt ^ ((r2 >> 1) & 3)) << 5) + 8 * pp);
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf, pf[t], acc[t][dt]);
+        }
+      }
+    };
+    for (int c = 0; c < nfull; ++c) {
+      if (first) block_ready(c);
+      if (DEBUG != 1) do_block(c, std::false_type{});
+    }
+    if (nfull < nch) {
+      if (first) block_ready(nfull);
+      if (DEBUG != 1) do_block(nfull, std::true_type{});
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float inv = 1.0f / xrow_sum(l_run[t]);
+      const int q = tl[t] * 16 + col;
+      if (q < L) {
+        bf16* orow = p.out + ((size_t)b * L + q) * p.ldo + h * DH;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const f32x4 v = acc[t][dt] * inv;
+          *reinterpret_cast<bf16x4*>(orow + dt * 16 + g * 4) = to_bf16x4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+  };
+
+  if (npass == 0) {   // no tiles: still join pass 0's per-block barriers
+    for (int c = 0; c < nch; ++c) block_ready(c);
+    return;
+  }
+  bf16x8 qf[2][2];
+  if (DEBUG != 2) {
+    asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]));
+  }
+  for (int pass = 0; pass < npass; ++pass) {
+    const int tl[2] = {wave + 8 * pass, wave + 8 * pass + 4};
+    const bool two = tl[1] < nqt;
+    if (pass == 0) {
+      if (DEBUG == 0) {
+        // Q (the oldest loads) retired together with block 0; "+v" keeps every consumer below the wait
+        wait_vmcnt_dyn(ops_after(0));
+        asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]));
+      } else if (DEBUG == 1) {
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]));
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) qf[t][ks] = __builtin_bit_cast(bf16x8, q0[t][ks]);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        qf[0][ks] = *reinterpret_cast<const bf16x8*>(qptr(tl[0], ks));
+        qf[1][ks] = *reinterpret_cast<const bf16x8*>(qptr(two ? tl[1] : tl[0], ks));
+      }
+    }
+    if (two) run_pass(std::integral_constant<int, 2>{}, qf, tl, pass == 0);
+    else run_pass(std::integral_constant<int, 1>{}, qf, tl, pass == 0);
+  }
+}
 }  // namespace
 
 const char* attention_check(const AttentionArgs& p) {
@@ -377,6 +637,21 @@ hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream) {
   // automatic choice stays on the streamed structure until the head-resident one has been measured on the
   // device (tools/attn_bench.py); both are covered by tests/test_gpu_kernels.py::test_attention_algos
   if (algo == 0) algo = 1;
+  if (algo >= 4 && algo <= 6 && p.Dh == 64 && Lp * 256 <= 80 * 1024) {
+    const int smem = Lp * 256;
+    static bool attr2 = false;
+    if (!attr2) {
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      attr2 = true;
+    }
+    if (algo == 4) hipLaunchKernelGGL(attention_v2_kernel<0>, dim3(p.B * p.H), dim3(256), smem, stream, p, nqt, Lp);
+    else if (algo == 5) hipLaunchKernelGGL(attention_v2_kernel<1>, dim3(p.B * p.H), dim3(256), smem, stream, p, nqt, Lp);
+    else hipLaunchKernelGGL(attention_v2_kernel<2>, dim3(p.B * p.H), dim3(256), smem, stream, p, nqt, Lp);
+    return hipGetLastError();
+  }
+  if (algo >= 4) algo = 1;
   if (algo == 2 || algo == 3) {
     const int T = algo;
     const int nw = (nqt + T - 1) / T;

@@ -241,7 +241,7 @@ def test_attention(lib, L, Dh):
     assert rel(out.float(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3])
+@pytest.mark.parametrize("algo", [1, 2, 3, 4])
 @pytest.mark.parametrize("L", [17, 66, 257, 258, 334, 590])
 def test_attention_algos(lib, algo, L):
     """Both attention structures (1: streamed K/V per 64-query block; 2/3: head-resident K/V, 2 or 3 query
