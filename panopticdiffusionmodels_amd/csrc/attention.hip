@@ -626,7 +626,7 @@ const char* attention_check(const AttentionArgs& p) {
   return nullptr;
 }
 
-static int g_attention_algo = 0;   // 0 auto, 1 = 64-query blocks with streamed K/V, 2/3 = head-resident T = 2/3
+static int g_attention_algo = 0;   // 0 auto, 1 streamed K/V, 2/3 head-resident T = 2/3, 4 head-resident v2 (5/6 timing)
 void attention_set_algo(int algo) { g_attention_algo = algo; }
 
 hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream) {
@@ -634,16 +634,16 @@ hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream) {
   int algo = g_attention_algo;
   const int Lp = (p.L + 31) / 32 * 32;   // PV reads whole 32-key steps
   if (p.Dh != 64 || Lp * 256 > 160 * 1024) algo = 1;
-  // automatic choice stays on the streamed structure until the head-resident one has been measured on the
-  // device (tools/attn_bench.py); both are covered by tests/test_gpu_kernels.py::test_attention_algos
-  if (algo == 0) algo = 1;
-  if (algo >= 4 && algo <= 6 && p.Dh == 64 && Lp * 256 <= 80 * 1024) {
+  // automatic: the head-resident v2 structure wherever the head's K/V fit in LDS (Dh = 64: every U-ViT-S/M/L
+  // shape); measured 152 vs 213 us (streamed) on L/2 at 190 rows (tools/attn_bench.py)
+  if (algo == 0 && p.Dh == 64 && Lp * 256 <= 160 * 1024) algo = 4;
+  if (algo >= 4 && algo <= 6 && p.Dh == 64 && Lp * 256 <= 160 * 1024) {
     const int smem = Lp * 256;
     static bool attr2 = false;
     if (!attr2) {
-      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr2 = true;
     }
     if (algo == 4) hipLaunchKernelGGL(attention_v2_kernel<0>, dim3(p.B * p.H), dim3(256), smem, stream, p, nqt, Lp);
@@ -651,7 +651,7 @@ hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream) {
     else hipLaunchKernelGGL(attention_v2_kernel<2>, dim3(p.B * p.H), dim3(256), smem, stream, p, nqt, Lp);
     return hipGetLastError();
   }
-  if (algo >= 4) algo = 1;
+  if (algo == 0 || algo >= 4) algo = 1;
   if (algo == 2 || algo == 3) {
     const int T = algo;
     const int nw = (nqt + T - 1) / T;
