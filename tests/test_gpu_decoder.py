@@ -60,13 +60,15 @@ def test_decoder_chunked_batch_vs_oracle(dev):
 
 
 def test_decoder_latent64_vs_oracle(dev):
-    """512x512 decode (latent 64, BASELINE configs[4]): 4096-token mid attention, 512^2 output."""
+    """512x512 decode (latent 64, BASELINE configs[4]) of two images in one chunk: 4096-token mid attention,
+    512^2 output, every image vs the oracle."""
     ae, sd = _ae(128, (1, 2, 4, 4), 2, 4, "reference", 64)
     g = torch.Generator().manual_seed(6)
-    z = torch.randn(1, 4, 64, 64, generator=g)
+    z = torch.randn(2, 4, 64, 64, generator=g)
     img = ae.to(dev).decode(z.to(dev))
-    assert img.shape == (1, 3, 512, 512)
-    assert rel(img, autoencoder_ref.decode(sd, z)) < TOL
+    assert img.shape == (2, 3, 512, 512)
+    for i in range(2):
+        assert rel(img[i:i + 1], autoencoder_ref.decode(sd, z[i:i + 1])) < TOL
 
 
 def test_decoder_rejects_unsupported(dev):
