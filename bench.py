@@ -11,8 +11,8 @@ latents over RCCL (N > 1) -> decode of the rank's own B latents.
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL over xGMI)
 
 Rank 0 prints one JSON line.  `value` = images/sec of the whole job = N*B*K / max-over-ranks wall time.
-The CPU baseline (rank 0, N = 1 only, after the GPU timing) times the fp32 CPU oracle on a bounded sample
-of the same workload (a few CFG forwards + one decode) and extrapolates to images/sec.
+The CPU baseline (rank 0, N = 1 only, after the GPU timing) times the fp32 CPU oracle on a bounded sample of the
+same workload: one full 50-NFE CFG sample of 2 images + their decode.
 """
 import argparse
 import json
@@ -32,6 +32,8 @@ from panopticdiffusionmodels_amd.sampler import ClassCondSampler  # noqa: E402
 from panopticdiffusionmodels_amd.utils import get_nnet  # noqa: E402
 
 PEAK_BF16 = 2.5e15   # dense bf16 MFMA, MI355X_MICROARCH.md chip table
+MODEL_NAMES = {"imagenet256_uvit_large": "U-ViT-L/2", "imagenet256_uvit_huge": "U-ViT-H/2",
+               "imagenet512_uvit_huge": "U-ViT-H/4", "cifar10_uvit_small": "U-ViT-S/2 (pixel)"}
 
 
 def parse():
@@ -45,7 +47,6 @@ def parse():
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    ap.add_argument("--cpu-nfe", type=int, default=4, help="CFG forwards timed for the CPU baseline")
     return ap.parse_args()
 
 
@@ -159,10 +160,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (seeded random-init U-ViT-L/2 + KL-f8 weights, z_T ~ N(0,1), labels U{0..999})",
+        "data": f"synthetic (seeded random-init {MODEL_NAMES.get(args.config, args.config)} + KL-f8 weights, "
+                "z_T ~ N(0,1), labels U{0..999})",
         "config": {"workload": f"{args.config}: 50-step DPM-Solver (fast, order 3), CFG {full['cfg_scale']}, "
                                f"{'+ KL-f8 decode 256x256' if ae is not None else 'no decode'}",
-                   "model": "U-ViT-L/2", "per_gpu_batch": B, "global_batch": world * B,
+                   "model": MODEL_NAMES.get(args.config, args.config), "per_gpu_batch": B, "global_batch": world * B,
                    "nfe": sampler.nfe, "hip_graph": not args.no_graph, "parallelism": f"dp{world} (batch-sharded)"},
         "roofline": roof,
         "breakdown_ms_per_step": {"sample_50nfe": round(samp_ms, 2), "decode": round(dec_ms, 2),
@@ -170,7 +172,7 @@ def main():
                                           "with per-GEMM events (graph replay in the others)"},
     }
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
-        res["cpu_baseline"] = cpu_baseline(full, ncfg, args.cpu_nfe, ae is not None)
+        res["cpu_baseline"] = cpu_baseline(full, ncfg, ae is not None)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -205,42 +207,63 @@ def gemm_roofline(prof, ncfg, rows):
             "flops_per_launch": round(tot_f / n), "flops_per_forward": gemm_flops_per_forward(ncfg, rows)}
 
 
-def cpu_baseline(full, ncfg, n_fwd, with_decode):
-    """fp32 CPU oracle (oracle/uvit_ref.py, oracle/autoencoder_ref.py) on the host cores, bounded sample:
-    `n_fwd` CFG forwards at 2 rows (1 image) + one 256x256 decode, extrapolated to 50 NFE per image."""
-    from oracle import autoencoder_ref, uvit_ref
+def cpu_baseline(full, ncfg, with_decode):
+    """The reference path timed on the host cores with the fp32 CPU oracle (oracle/uvit_ref.py, solver_ref.py,
+    autoencoder_ref.py), SURVEY.md §8d: one FULL 50-NFE sample of B = 2 images through the reference's own
+    solver front end and CFG closure (eval_ldm.py:66-108: cond and uncond as two B-row forwards per NFE), then
+    the KL-f8 decode of both images.  Threads: the process's CPU affinity, capped by OMP_NUM_THREADS (the GPU
+    box sets 16 = this job's CPU share; os.cpu_count() there reports the whole machine)."""
+    from oracle import autoencoder_ref, solver_ref, uvit_ref
     cores = len(os.sched_getaffinity(0))
-    cores = min(cores, 16)   # the GPU box's CPU share
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))
     torch.set_num_threads(cores)
     kw = dict(ncfg)
     kw.pop("name")
     sd = weights.nnet_state_dict(ncfg, seed=0, init="reference")
+    B = 2
     g = torch.Generator().manual_seed(0)
-    x = torch.randn(2, *full["z_shape"], generator=g)
-    y = torch.tensor([1, 1000])
-    t = torch.full((2,), 500.0)
+    z = torch.randn(B, *full["z_shape"], generator=g)
+    null = ncfg["num_classes"] - 1
+    y = torch.randint(0, null, (B,), generator=g)
+
+    def nnet(x, t, yy):
+        return uvit_ref.uvit_forward(sd, kw, x, t, yy)
+    nfe = [0]
+
+    def counted(fn):
+        def f(*a):
+            nfe[0] += 1
+            return fn(*a)
+        return f
     with torch.no_grad():
-        uvit_ref.uvit_forward(sd, kw, x, t, y)  # warm-up
-        t0 = time.perf_counter()
-        for _ in range(n_fwd):
-            uvit_ref.uvit_forward(sd, kw, x, t, y)
-        t_fwd = (time.perf_counter() - t0) / n_fwd
+        nnet(z, torch.full((B,), 500.0), y)   # warm-up (allocator, thread pool)
+        if full["front_end"] == "dpm_solver_pytorch":
+            model = counted(solver_ref.cfg_class_closure(nnet, y, full["cfg_scale"], null, 999))
+            t0 = time.perf_counter()
+            lat = solver_ref.pytorch_sample(model, z, steps=full["sample_steps"], eps=full.get("eps", 1e-4))
+        else:
+            fn = counted(solver_ref.cfg_class_closure(nnet, y, full["cfg_scale"], null, 1000))
+            t0 = time.perf_counter()
+            lat, _ = solver_ref.pp_sample(lambda x, t, mt: (fn(x, t), None), solver_ref.sd_betas(), z,
+                                          steps=full["sample_steps"])
+        t_sample = time.perf_counter() - t0
         t_dec = 0.0
         if with_decode:
             dsd = weights.decoder_state_dict(seed=1)
-            z = torch.randn(1, 4, 32, 32, generator=g)
             t0 = time.perf_counter()
-            autoencoder_ref.decode(dsd, z)
+            autoencoder_ref.decode(dsd, lat)
             t_dec = time.perf_counter() - t0
-    per_img = full["sample_steps"] * t_fwd + t_dec
+    assert torch.isfinite(lat).all()
     try:
-        model = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":", 1)[1].strip()
+        model_name = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":", 1)[1].strip()
     except Exception:
-        model = "unknown"
-    return {"value": round(1.0 / per_img, 5), "unit": "images/sec", "cores": cores, "kind": "port",
-            "cpu": model,
-            "sample": f"{n_fwd} CFG forwards of U-ViT-L/2 at 2 rows (1 image) = {t_fwd:.3f} s each, "
-                      f"+ 1 KL-f8 decode 256x256 = {t_dec:.2f} s; images/sec = 1 / (50 NFE x forward + decode)"}
+        model_name = "unknown"
+    return {"value": round(B / (t_sample + t_dec), 5), "unit": "images/sec", "cores": cores, "kind": "port",
+            "cpu": model_name,
+            "sample": f"one full {nfe[0]}-NFE {full['front_end']} sample of B={B} images (CFG {full['cfg_scale']}: "
+                      f"cond + uncond forwards of {B} rows per NFE) = {t_sample:.1f} s, + KL-f8 decode of {B} "
+                      f"images = {t_dec:.1f} s; images/sec = {B} / total"}
 
 
 if __name__ == "__main__":
