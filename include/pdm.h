@@ -138,6 +138,29 @@ int pdm_gemm_bf16_ln(const void* A, int lda, const void* W, const float* bias, i
                      const float* ln_stats, const float* ln_colsum, float ln_eps, void* stream);
 /* LayerNorm partials of fp32 rows (as above) + optional bf16 copy xb [rows][D] */
 int pdm_rowstats(const float* x, int ldx, int rows, int D, void* xb, float* stats, void* stream);
+/* General GEMM entry (every operand / epilogue option of the kernels; the fixed-signature entries above are
+ * shorthands).  fp8 != 0: A1 / W are MXFP8 e4m3 bytes with E8M0 block-scale dwords a_scale [K/128][a_scale_ld]
+ * / w_scale [K/128][w_scale_ld] (byte j of dword (kt, row) scales K block kt*4 + j, 32 elements), computed on
+ * v_mfma_scale_f32_16x16x128_f8f6f4.  out_fp8 != NULL: the epilogue also writes its stored values in MXFP8
+ * (e4m3 [M][ldo8] + scales [N/128][out_scale_ld], exponent ceil(log2(amax/448)) per 32 columns).  LayerNorm
+ * producer / consumer fields as pdm_gemm_bf16_ln. */
+typedef struct pdm_gemm_args {
+  const void* A1; int lda1;
+  const void* A2; int lda2; int K1;
+  const void* W; int ldw;
+  const float* bias;
+  int M, N, K;
+  void* out_bf16; int ldo;
+  float* out_f32; int ldr; int accumulate;
+  float* stats_out;
+  const float* ln_stats; const float* ln_colsum; float ln_eps;
+  int fp8;
+  const unsigned* a_scale; int a_scale_ld;
+  const unsigned* w_scale; int w_scale_ld;
+  void* out_fp8; int ldo8;
+  unsigned* out_scale; int out_scale_ld;
+} pdm_gemm_args;
+int pdm_gemm(const pdm_gemm_args* a, int epi, void* stream);
 /* Implicit-GEMM conv3x3 (stride 1, pad 1) on NHWC bf16 input [B, H>>up, W>>up, Cin] (up = 1: the nearest-x2
  * upsample of libs/autoencoder.py:35-50 folded into the addressing); Wt [N][9*Cin] in (ky, kx, ci) order;
  * output rows = output pixels (b, y, x), N channels (libs/autoencoder.py ResnetBlock conv1/conv2, Upsample.conv) */

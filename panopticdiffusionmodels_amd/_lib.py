@@ -41,6 +41,20 @@ class PdmStageEpilogueArgs(ctypes.Structure):
     ]
 
 
+class PdmGemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("A1", ctypes.c_void_p), ("lda1", ctypes.c_int), ("A2", ctypes.c_void_p), ("lda2", ctypes.c_int),
+        ("K1", ctypes.c_int), ("W", ctypes.c_void_p), ("ldw", ctypes.c_int), ("bias", ctypes.c_void_p),
+        ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int),
+        ("out_bf16", ctypes.c_void_p), ("ldo", ctypes.c_int), ("out_f32", ctypes.c_void_p), ("ldr", ctypes.c_int),
+        ("accumulate", ctypes.c_int), ("stats_out", ctypes.c_void_p), ("ln_stats", ctypes.c_void_p),
+        ("ln_colsum", ctypes.c_void_p), ("ln_eps", ctypes.c_float), ("fp8", ctypes.c_int),
+        ("a_scale", ctypes.c_void_p), ("a_scale_ld", ctypes.c_int), ("w_scale", ctypes.c_void_p),
+        ("w_scale_ld", ctypes.c_int), ("out_fp8", ctypes.c_void_p), ("ldo8", ctypes.c_int),
+        ("out_scale", ctypes.c_void_p), ("out_scale_ld", ctypes.c_int),
+    ]
+
+
 _SIGS = {
     "pdm_last_error": (ctypes.c_char_p, []),
     "pdm_version": (ctypes.c_int, []),
@@ -74,6 +88,7 @@ _SIGS = {
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_void_p]),
+    "pdm_gemm": (ctypes.c_int, [ctypes.POINTER(PdmGemmArgs), ctypes.c_int, ctypes.c_void_p]),
     "pdm_gemm_bf16_ln": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -207,6 +222,63 @@ def gemm_ln(a, w, bias, epi, ln_stats=None, ln_colsum=None, out=None, out_f32=No
                                ptr(ln_stats), ptr(ln_colsum), eps, stream_ptr(a.device)), "pdm_gemm_bf16_ln")
     res = out_f32 if epi == EPI_F32 else out
     return (res, st) if stats_out else res
+
+
+# ---- MXFP8 (OCP e4m3 + E8M0 per 32 elements) host reference and GEMM wrapper --------------------------
+
+def mx_quantize(x):
+    """MXFP8 of x [R, K] (K % 128 == 0) exactly as the GPU epilogue quantises (csrc/pdm_common.h mx_quant8):
+    E8M0 exponent e = ceil(log2(amax/448)) + 127 per 32 consecutive elements, e4m3 = RNE(x * 2^(127 - e)).
+    Returns (q [R, K] float8_e4m3fn, scale dwords [K/128, R] int32: byte j of (kt, r) = block kt*4 + j)."""
+    R, K = x.shape
+    xb = x.float().reshape(R, K // 32, 32)
+    amax = xb.abs().amax(-1)
+    bits = (amax * (1.0 / 448.0)).view(torch.int32)
+    e = ((bits >> 23) & 0xFF) + ((bits & 0x7FFFFF) != 0).to(torch.int32)
+    e = e.clamp(max=254)
+    inv = ((254 - e) << 23).view(torch.float32)
+    q = (xb * inv[..., None]).reshape(R, K).to(torch.float8_e4m3fn)
+    sc = e.to(torch.uint8).reshape(R, K // 128, 4).permute(1, 0, 2).contiguous().view(torch.int32).reshape(K // 128, R)
+    return q, sc
+
+
+def mx_dequantize(q, sc):
+    R, K = q.shape
+    e = sc.contiguous().view(torch.uint8).reshape(K // 128, R, 4).permute(1, 0, 2).reshape(R, K // 32).to(torch.int32)
+    scale = torch.pow(2.0, (e - 127).double()).float()
+    return (q.float().reshape(R, K // 32, 32) * scale[..., None]).reshape(R, K)
+
+
+def gemm_ex(epi, a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=None, accumulate=False,
+            ln_stats=None, ln_colsum=None, stats_out=None, out_fp8=None, out_scale=None, eps=1e-5):
+    """pdm_gemm with every option (include/pdm.h pdm_gemm_args).  a / w are bf16, or float8_e4m3fn with their
+    scale dword arrays (MXFP8)."""
+    lib = load()
+    require_gpu(a)
+    M, K = a.shape
+    N = w.shape[0]
+    g = PdmGemmArgs()
+    g.A1, g.lda1 = a.data_ptr(), a.stride(0)
+    g.W, g.ldw = w.data_ptr(), w.stride(0)
+    g.bias = bias.data_ptr() if bias is not None else None
+    g.M, g.N, g.K = M, N, K
+    if out is not None:
+        g.out_bf16, g.ldo = out.data_ptr(), out.stride(0)
+    if out_f32 is not None:
+        g.out_f32, g.ldr = out_f32.data_ptr(), out_f32.stride(0)
+    g.accumulate = int(accumulate)
+    g.stats_out = stats_out.data_ptr() if stats_out is not None else None
+    g.ln_stats = ln_stats.data_ptr() if ln_stats is not None else None
+    g.ln_colsum = ln_colsum.data_ptr() if ln_colsum is not None else None
+    g.ln_eps = eps
+    if a.dtype == torch.float8_e4m3fn:
+        g.fp8 = 1
+        g.a_scale, g.a_scale_ld = a_scale.data_ptr(), a_scale.shape[1]
+        g.w_scale, g.w_scale_ld = w_scale.data_ptr(), w_scale.shape[1]
+    if out_fp8 is not None:
+        g.out_fp8, g.ldo8 = out_fp8.data_ptr(), out_fp8.stride(0)
+        g.out_scale, g.out_scale_ld = out_scale.data_ptr(), out_scale.shape[1]
+    check(lib.pdm_gemm(ctypes.byref(g), epi, stream_ptr(a.device)), "pdm_gemm")
 
 
 def gemm_conv3x3(x, w, bias=None, epi=EPI_F32, up=0, out=None, out_f32=None, accumulate=False):

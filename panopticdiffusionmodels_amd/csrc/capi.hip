@@ -716,6 +716,28 @@ int pdm_rowstats(const float* x, int ldx, int rows, int D, void* xb, float* stat
   return PDM_OK;
 }
 
+int pdm_gemm(const pdm_gemm_args* g, int epi, void* stream) {
+  if (!g) return fail(PDM_ERR_ARG, "pdm_gemm: null args");
+  pdm::GemmArgs a{};
+  a.A1 = (const bf16*)g->A1; a.lda1 = g->lda1;
+  a.A2 = (const bf16*)g->A2; a.lda2 = g->lda2;
+  a.K1 = g->A2 ? g->K1 : g->K;
+  a.W = (const bf16*)g->W; a.ldw = g->ldw; a.bias = g->bias;
+  a.M = g->M; a.N = g->N; a.K = g->K;
+  a.out_bf16 = (bf16*)g->out_bf16; a.ldo = g->ldo;
+  a.out_f32 = g->out_f32; a.ldr = g->ldr; a.accumulate = g->accumulate;
+  a.stats_out = g->stats_out; a.stats_ld = (g->N + 255) / 256;
+  a.ln_stats = g->ln_stats; a.ln_ld = (g->K + 255) / 256; a.ln_D = g->K; a.ln_eps = g->ln_eps; a.ln_colsum = g->ln_colsum;
+  a.fp8 = g->fp8;
+  a.a_scale = g->a_scale; a.a_scale_ld = g->a_scale_ld;
+  a.w_scale = g->w_scale; a.w_scale_ld = g->w_scale_ld;
+  a.out_fp8 = (unsigned char*)g->out_fp8; a.ldo8 = g->ldo8;
+  a.out_scale = g->out_scale; a.out_scale_ld = g->out_scale_ld;
+  PDM_CHECK(pdm::gemm_check(a, epi));
+  PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
+  return PDM_OK;
+}
+
 int pdm_gemm_conv3x3_bf16(const void* in, int B, int H, int W, int Cin, int up, const void* Wt, const float* bias,
                           int N, int epi, void* out_bf16, float* out_f32, int accumulate, void* stream) {
   static bf16* zero = nullptr;   // zero page for the tile policies that address padded taps explicitly

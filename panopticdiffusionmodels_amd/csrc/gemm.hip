@@ -12,6 +12,7 @@
 // ds_read_b128 fragment read bank-conflict free.  The MFMA is issued with the weight fragment as the A
 // operand so each lane ends up owning 4 consecutive output columns of one row: 8/16-byte epilogue stores.
 #include <type_traits>
+#include <utility>
 
 #include "pdm_common.h"
 #include "pdm_kernels.h"
@@ -283,6 +284,21 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
       const int ml = idx >> 5, ch = idx & 31;
       v[it] = *reinterpret_cast<const i32x4*>(smem + ml * 512 + ((ch ^ (ml & 31)) << 4));
     }
+    if (p.out_fp8) {   // MXFP8 copy: 4 consecutive lanes hold one 32-column block of a row
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int idx = it * 512 + tid;
+        const int m = m0 + (idx >> 5), n = n0 + (idx & 31) * 8;
+        const bf16x8 b8 = __builtin_bit_cast(bf16x8, v[it]);
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (float)b8[j];
+        unsigned e8;
+        const uint2 q = mx_quant8(f, &e8);
+        if (m < p.M && n < p.N) mx_store8(p.out_fp8, p.ldo8, p.out_scale, p.out_scale_ld, m, n, q, e8, (tid & 3) == 0);
+      }
+    }
+    if (!p.out_bf16) return;
     if (full) {
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
@@ -324,6 +340,12 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
     for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
     if ((tid & 31) == 0 && m < p.M)
       *reinterpret_cast<float2*>(p.stats_out + ((size_t)m * p.stats_ld + (n0 >> 8)) * 2) = make_float2(sv, q);
+  };
+  auto mx_row = [&](const f32x4& a, const f32x4& b, int m, int n) {   // MXFP8 copy of the stored fp32 row piece
+    const float f[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    unsigned e8;
+    const uint2 q = mx_quant8(f, &e8);
+    if (m < p.M && n < p.N) mx_store8(p.out_fp8, p.ldo8, p.out_scale, p.out_scale_ld, m, n, q, e8, (tid & 3) == 0);
   };
   f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
   if (p.bias) {
@@ -387,6 +409,13 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
             row_stats(v0[i], v1[i], m0 + pass * 128 + (idx >> 5), n0 + (idx & 31) * 8);
           }
         }
+        if (p.out_fp8) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int idx = (g * 4 + i) * 512 + tid;
+            mx_row(v0[i], v1[i], m0 + pass * 128 + (idx >> 5), n0 + (idx & 31) * 8);
+          }
+        }
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -411,6 +440,7 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
             v1[i] = b;
           }
           if (p.stats_out) row_stats(v0[i], v1[i], m, n);
+          if (p.out_fp8) mx_row(v0[i], v1[i], m, n);
         }
       }
     }
@@ -989,6 +1019,213 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
 
   epilogue256<EPI, 1>(p, acc, smem, m0, n0, tid, lane, wm, wn);
 }
+
+// ------------------------------------------------------------------------------------------------
+// MXFP8 GEMM (algo 7 schedule, e4m3 operands with E8M0 block scales) on v_mfma_scale_f32_16x16x128_f8f6f4:
+// twice the bf16 MFMA rate.  A K-tile is 128 fp8 = 128-byte LDS rows, so staging, swizzle and fragment reads
+// are byte-for-byte those of the bf16 kernel (a lane's 32-byte fragment = chunks g and 4+g, g = lane >> 4,
+// exactly the operand layout the scaled MFMA expects: tools/probes/mx_layout.hip).  Per K-tile each wave also
+// stages 256 B of block scales (waves 0-3: A rows, waves 4-7: W rows) into a 2 KiB slot; a lane packs the four
+// E8M0 bytes it needs per operand half into one VGPR and the MFMA selects them with opsel.
+//   phase A(k): reads A0 W0 W1 + scales of tile k, issues A1(k+1)          wait: A1(k)
+//   phase B(k): reads A1,      issues S A0 W0 W1 of tile k+2               wait: S A0 W0 W1 (k+1)
+template <int... I, class F>
+__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  sfor_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+constexpr int MX_SCALE_LDS = EPI_LDS + EPI_LDS_EXTRA;   // 2 x 2 KiB of staged block scales
+constexpr int MX_SMEM = MX_SCALE_LDS + 2 * 2048;
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_mx_kernel(GemmArgs p, int tiles_n, int nwg) {
+  constexpr int HALF = 128 * 128;
+  constexpr int BUF = 4 * HALF;
+  enum { KA0 = 0, KA1 = 1, KW0 = 2, KW1 = 3 };
+  typedef int v8i __attribute__((ext_vector_type(8)));
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: scalar descriptor choice
+  const int wm = wave >> 2, wn = wave & 3, g = lane >> 4;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+  }
+  int tm, tn;
+  if (p.raster > 0) {
+    const int tiles_m = (p.M + BM2 - 1) / BM2;
+    const int grp = bid / (p.raster * tiles_n);
+    const int rows_in = min(p.raster, tiles_m - grp * p.raster);
+    const int r = bid - grp * p.raster * tiles_n;
+    tm = grp * p.raster + r % rows_in;
+    tn = r / rows_in;
+  } else {
+    tm = bid / tiles_n;
+    tn = bid - tm * tiles_n;
+  }
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int ldw = p.ldw > 0 ? p.ldw : p.K;
+  const int nk = p.K / 128;
+  const unsigned char* A8 = reinterpret_cast<const unsigned char*>(p.A1);
+  const unsigned char* W8 = reinterpret_cast<const unsigned char*>(p.W);
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A8, (long long)p.M * p.lda1);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(W8, (long long)(p.N - 1) * ldw + p.K);
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(p.a_scale, (long long)nk * p.a_scale_ld * 4);
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.w_scale, (long long)nk * p.w_scale_ld * 4);
+
+  const int prow = lane >> 3, pch = lane & 7;
+  unsigned aoff[2][2], woff[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + prow;
+    const unsigned sb = (unsigned)((pch ^ ((row >> 1) & 7)) * 16);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int gm = m0 + h * 128 + row, gn = n0 + h * 128 + row;
+      aoff[h][i] = gm < p.M ? (unsigned)gm * (unsigned)p.lda1 + sb : OOB;
+      woff[h][i] = gn < p.N ? (unsigned)gn * (unsigned)ldw + sb : OOB;
+    }
+  }
+  // block-scale staging: wave w < 4 stages A rows m0 + 64 w + lane, waves 4-7 W rows n0 + 64 (w - 4) + lane
+  const bool s_is_a = wave < 4;
+  const int srow = (wave & 3) * 64 + lane;
+  const unsigned soff = s_is_a ? (m0 + srow < p.M ? (unsigned)(m0 + srow) * 4u : OOB)
+                               : (n0 + srow < p.N ? (unsigned)(n0 + srow) * 4u : OOB);
+
+  auto issue = [&](int kt, int kind) {
+    char* dst = smem + (kt & 1) * BUF + kind * HALF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      PDM_LDS void* d = (PDM_LDS void*)(dst + (wave * 2 + i) * 1024);
+      if (kind >= KW0) dma16(rw, woff[kind - KW0][i], kt * 128, d);
+      else dma16(ra, aoff[kind][i], kt * 128, d);
+    }
+  };
+  auto issue_scales = [&](int kt) {
+    PDM_LDS void* d = (PDM_LDS void*)(smem + MX_SCALE_LDS + (kt & 1) * 2048 + (s_is_a ? 0 : 1024) + (wave & 3) * 256);
+    if (s_is_a) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, d, 4, (int)soff, kt * p.a_scale_ld * 4, 0, 0);
+    else __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, d, 4, (int)soff, kt * p.w_scale_ld * 4, 0, 0);
+  };
+
+  f32x4 acc[32];
+#pragma unroll
+  for (int f = 0; f < 32; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  v8i af[4];        // A fragments of the current A half: [mi], 32 fp8 each
+  v8i wf[2][2];     // W fragments of both W halves: [qj][ni]
+  unsigned sa[2], sw = 0;   // packed E8M0: sa[qi] byte mi, sw byte qj*2 + ni
+
+  // a lane's 32-byte fragment = its row's 16-byte chunks g and 4 + g, read straight into the 8-VGPR operand
+  auto frag = [&](v8i& dst, const char* base, int row) {
+    i32x4* h = reinterpret_cast<i32x4*>(&dst);
+    h[0] = *reinterpret_cast<const i32x4*>(base + swz_off<64>(row, g));
+    h[1] = *reinterpret_cast<const i32x4*>(base + swz_off<64>(row, 4 + g));
+  };
+  auto read_a = [&](const char* buf, int qi) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) frag(af[mi], buf + qi * HALF, wm * 64 + mi * 16 + (lane & 15));
+  };
+  auto read_w = [&](const char* buf) {
+#pragma unroll
+    for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) frag(wf[qj][ni], buf + (2 + qj) * HALF, wn * 32 + ni * 16 + (lane & 15));
+  };
+  auto read_scales = [&](int kt) {
+    const unsigned* sl = reinterpret_cast<const unsigned*>(smem + MX_SCALE_LDS + (kt & 1) * 2048);
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+      unsigned v = 0;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+        v |= ((sl[qi * 128 + wm * 64 + mi * 16 + (lane & 15)] >> (8 * g)) & 0xffu) << (8 * mi);
+      sa[qi] = v;
+    }
+    unsigned v = 0;
+#pragma unroll
+    for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        v |= ((sl[256 + qj * 128 + wn * 32 + ni * 16 + (lane & 15)] >> (8 * g)) & 0xffu) << (8 * (qj * 2 + ni));
+    sw = v;
+    asm volatile("" : "+v"(sa[0]), "+v"(sa[1]), "+v"(sw));
+  };
+  auto lds_done = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mma = [&](auto qic, auto qjc) {
+    constexpr int qi = decltype(qic)::value, qj = decltype(qjc)::value;
+    __builtin_amdgcn_s_setprio(1);
+    static_for<2>([&](auto nic) {
+      constexpr int ni = decltype(nic)::value;
+      static_for<4>([&](auto mic) {
+        constexpr int mi = decltype(mic)::value;
+        f32x4& c = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
+        c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[qj][ni], af[mi], c, 0, 0, qj * 2 + ni, sw, mi,
+                                                             sa[qi]);
+        // pin the MFMA inside this phase: IR-level sinking otherwise moves whole MFMA clusters (and the scale
+        // packing feeding them) across the barriers into the next phase
+        asm volatile("" : "+v"(c));
+      });
+    });
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  issue_scales(0);
+  issue(0, KA0);
+  issue(0, KW0);
+  issue(0, KW1);
+  issue(0, KA1);
+  if (nk > 1) {
+    issue_scales(1);
+    issue(1, KA0);
+    issue(1, KW0);
+    issue(1, KW1);
+    asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  }
+  bar_raw();
+  if (wave >= 4) bar_raw();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* buf = smem + (kt & 1) * BUF;
+    const bool m1 = kt + 1 < nk, m2 = kt + 2 < nk;
+    // phase A
+    read_a(buf, 0);
+    read_w(buf);
+    read_scales(kt);
+    lds_done();
+    if (m1) { issue(kt + 1, KA1); asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); }   // A1(kt)
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar_raw();
+    mma(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    mma(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+    bar_raw();
+    // phase B
+    read_a(buf, 1);
+    lds_done();
+    if (m2) {
+      issue_scales(kt + 2);
+      issue(kt + 2, KA0);
+      issue(kt + 2, KW0);
+      issue(kt + 2, KW1);
+      asm volatile("s_waitcnt vmcnt(9)" ::: "memory");   // S A0 W0 W1 (kt+1)
+    } else if (m1) {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
+    bar_raw();
+    mma(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+    mma(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+    bar_raw();
+  }
+  if (wave < 4) bar_raw();
+  epilogue256<EPI, 1>(p, acc, smem, m0, n0, tid, lane, wm, wn);
+}
 }  // namespace
 
 const char* gemm_check(const GemmArgs& p, int epi) {
@@ -1010,6 +1247,15 @@ const char* gemm_check(const GemmArgs& p, int epi) {
   if (p.stats_out && (epi != EPI_F32 || p.stats_ld < (p.N + 255) / 256 || ((uintptr_t)p.stats_out & 7)))
     return "gemm: LayerNorm stats need the fp32 epilogue and stats_ld >= ceil(N / 256)";
   if ((p.stats_out || p.ln_stats) && p.batch > 1) return "gemm: fused LayerNorm is not available for batched GEMMs";
+  if (p.out_fp8 && (p.N % 32 || p.ldo8 % 16 || !p.out_scale || p.out_scale_ld < p.M || p.batch > 1 ||
+                    ((uintptr_t)p.out_fp8 & 15) || ((uintptr_t)p.out_scale & 3)))
+    return "gemm: MXFP8 output needs N % 32 == 0, ldo8 % 16 == 0, a scale array with out_scale_ld >= M";
+  if (p.fp8) {
+    if (p.K % 128 || p.K1 != p.K || p.A2 || p.conv || p.a_rows_per_group || p.batch > 1)
+      return "gemm(fp8): K must be a multiple of 128; no split-K, conv, row gather or batch";
+    if (!p.a_scale || !p.w_scale || p.a_scale_ld < p.M || p.w_scale_ld < p.N || (p.lda1 % 16) || (p.ldw && p.ldw % 16))
+      return "gemm(fp8): block scales missing or leading dimensions not multiples of 16 bytes";
+  }
   if (p.ln_stats) {
     if (epi == EPI_F32) return "gemm: the fused LayerNorm applies to the bf16 / GELU epilogues";
     if (!p.ln_colsum || ((uintptr_t)p.ln_colsum & 15) || p.ln_D <= 0 || p.ln_ld != (p.ln_D + 255) / 256)
@@ -1094,6 +1340,25 @@ static hipError_t launch8d(const GemmArgs& p, int epi, hipStream_t stream) {
   return hipGetLastError();
 }
 
+static hipError_t launch_mx(const GemmArgs& p, int epi, hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_mx_kernel<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, MX_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm_mx_kernel<EPI_GELU>, hipFuncAttributeMaxDynamicSharedMemorySize, MX_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm_mx_kernel<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, MX_SMEM);
+    attr_set = true;
+  }
+  const int tn = (p.N + BN2 - 1) / BN2, tm = (p.M + BM2 - 1) / BM2;
+  const int nwg = tm * tn;
+  dim3 grid(nwg), block(512);
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL(gemm_mx_kernel<EPI_BF16>, grid, block, MX_SMEM, stream, p, tn, nwg); break;
+    case EPI_GELU: hipLaunchKernelGGL(gemm_mx_kernel<EPI_GELU>, grid, block, MX_SMEM, stream, p, tn, nwg); break;
+    default: hipLaunchKernelGGL(gemm_mx_kernel<EPI_F32>, grid, block, MX_SMEM, stream, p, tn, nwg); break;
+  }
+  return hipGetLastError();
+}
+
 // The descriptor-addressed kernel needs every operand byte offset below 2^31 (32-bit per-lane offsets).
 static bool fits_rsrc(const GemmArgs& p) {
   const long long lim = 0x7fffffffLL;
@@ -1119,6 +1384,11 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
   if ((epi == EPI_BF16 || epi == EPI_GELU) && (p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))) algo = 1;
   if (epi == EPI_F32 && (p.N % 8 || p.ldr % 4 || ((uintptr_t)p.out_f32 & 15) ||
                          (p.out_bf16 && (p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))))) algo = 1;
+  if (p.fp8) {
+    if (!fits_rsrc(p)) return hipErrorInvalidValue;
+    return launch_mx(p, epi, stream);
+  }
+  if (p.out_fp8) algo = 7;   // MXFP8 output lives in the 256-tile epilogue
   if (algo >= 5 && fits_rsrc(p)) {
     if (algo == 5) return p.conv ? launch8d<1, 0>(p, epi, stream) : launch8d<0, 0>(p, epi, stream);
     if (algo == 6) return p.conv ? launch8d<1, 1>(p, epi, stream) : launch8d<0, 1>(p, epi, stream);

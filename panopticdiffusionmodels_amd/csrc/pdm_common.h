@@ -71,6 +71,39 @@ __device__ __forceinline__ float2 ln_merge(const float* st, int T, int D, float 
   return make_float2(mean, 1.0f / sqrtf(m2 / (float)D + eps));
 }
 
+// MXFP8 quantisation of one 32-element block spread over 4 consecutive lanes (8 values each, lane & 3 =
+// position in the block): E8M0 exponent e = ceil(log2(amax / 448)) + 127 (so |v| 2^-(e-127) <= 448, no
+// saturation), e4m3 data with round-to-nearest-even (v_cvt_pk_fp8_f32, OCP e4m3 on gfx950).  Returns the 8
+// packed bytes; *e8 receives the block's biased exponent.
+__device__ __forceinline__ uint2 mx_quant8(const float (&v)[8], unsigned* e8) {
+  float am = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(v[j]));
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  const unsigned bits = __float_as_uint(am * (1.0f / 448.0f));
+  unsigned e = (bits >> 23) & 0xffu;
+  e += (bits & 0x7fffffu) ? 1u : 0u;
+  e = e > 254u ? 254u : e;
+  const float inv = __uint_as_float((254u - e) << 23);   // 2^(127 - e)
+  int w0 = 0, w1 = 0;
+  w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, w0, false);
+  w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, w0, true);
+  w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, w1, false);
+  w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, w1, true);
+  *e8 = e;
+  return make_uint2((unsigned)w0, (unsigned)w1);
+}
+
+// store of one quantised 8-column piece (row m, columns n .. n+7) of an MXFP8 output, and of its block scale
+// by the block's first lane
+__device__ __forceinline__ void mx_store8(unsigned char* out, int ldo8, unsigned* scale, int scale_ld, int m, int n,
+                                          uint2 q, unsigned e8, bool first) {
+  *reinterpret_cast<uint2*>(out + (size_t)m * ldo8 + n) = q;
+  if (first)
+    reinterpret_cast<unsigned char*>(scale)[((size_t)(n >> 7) * scale_ld + m) * 4 + ((n >> 5) & 3)] = (unsigned char)e8;
+}
+
 __device__ __forceinline__ bf16x4 to_bf16x4(float a, float b, float c, float d) {
   bf16x4 r;
   r[0] = (bf16)a; r[1] = (bf16)b; r[2] = (bf16)c; r[3] = (bf16)d;

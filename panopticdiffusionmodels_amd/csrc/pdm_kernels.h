@@ -39,6 +39,18 @@ struct GemmArgs {
   //    with mean_m / rstd_m merged from the ln_D-column row's partials (Chan), eps ln_eps
   float* stats_out; int stats_ld;
   const float* ln_stats; int ln_ld; int ln_D; float ln_eps; const float* ln_colsum;
+  // MXFP8 (OCP e4m3 data + one E8M0 scale per 32 consecutive K elements, the block-scaled MFMA
+  // v_mfma_scale_f32_16x16x128_f8f6f4): fp8 != 0 -> A1 [M][lda1] and W [N][ldw] are e4m3 bytes (split-K, conv
+  // and row gather unsupported) and a_scale / w_scale hold the E8M0 exponents as dwords
+  // [K/128][a_scale_ld >= M] / [K/128][w_scale_ld >= N], byte j of dword (kt, row) = block kt*4 + j.
+  int fp8;
+  const unsigned* a_scale; int a_scale_ld;
+  const unsigned* w_scale; int w_scale_ld;
+  // MXFP8 output (any epilogue): the stored values (the bf16 / GELU result, or the fp32 residual row) also
+  // quantised to e4m3 [M][ldo8] with E8M0 scales [N/128][out_scale_ld >= M] in the layout above (scale
+  // 2^ceil(log2(amax/448)) per 32 columns, so no element saturates)
+  unsigned char* out_fp8; int ldo8;
+  unsigned* out_scale; int out_scale_ld;
   // tuning knobs (set by gemm_launch): raster = row panels per tile group inside an XCD's range (0: row-major);
   // dbg_tile0 = stage every tile's operands from tile (0, 0) (timing experiments only: wrong results)
   int raster, dbg_tile0;
