@@ -32,6 +32,7 @@ from panopticdiffusionmodels_amd.sampler import ClassCondSampler  # noqa: E402
 from panopticdiffusionmodels_amd.utils import get_nnet  # noqa: E402
 
 PEAK_BF16 = 2.5e15   # dense bf16 MFMA, MI355X_MICROARCH.md chip table
+PEAK_FP8 = 5.0e15    # dense MX-fp8 (block-scaled 16x16x128 f8f6f4) MFMA, same table
 MODEL_NAMES = {"imagenet256_uvit_large": "U-ViT-L/2", "imagenet256_uvit_huge": "U-ViT-H/2",
                "imagenet512_uvit_huge": "U-ViT-H/4", "cifar10_uvit_small": "U-ViT-S/2 (pixel)"}
 
@@ -80,6 +81,8 @@ def main():
     net = get_nnet(**ncfg).to(dev).eval()
     net.load_state_dict(sd)
     del sd
+    precision = full.get("precision", "bf16")   # configs[4]: MXFP8 block Linears (UViT.set_precision)
+    net.set_precision(precision)
     null_label = ncfg["num_classes"] - 1 if ncfg.get("num_classes", -1) > 0 else None
     sampler = ClassCondSampler(net, front_end=full["front_end"], cfg_scale=full["cfg_scale"], null_label=null_label,
                                steps=full["sample_steps"], eps=full.get("eps"), use_graph=not args.no_graph)
@@ -142,7 +145,7 @@ def main():
 
     # ---- roofline of the dominant kernel (the bf16 GEMM family): HIP events recorded by libpdm on the launch
     # stream around every GEMM launch of the last forward of the last timed step
-    roof = gemm_roofline(prof, ncfg, 2 * B if sampler.cfg else B)
+    roof = gemm_roofline(prof, ncfg, 2 * B if sampler.cfg else B, precision)
     samp_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
 
@@ -159,11 +162,11 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "bf16" if precision == "bf16" else "mxfp8-e4m3 (qkv/proj/fc1/fc2) + bf16",
         "data": f"synthetic (seeded random-init {MODEL_NAMES.get(args.config, args.config)} + KL-f8 weights, "
                 "z_T ~ N(0,1), labels U{0..999})",
         "config": {"workload": f"{args.config}: 50-step DPM-Solver (fast, order 3), CFG {full['cfg_scale']}, "
-                               f"{'+ KL-f8 decode 256x256' if ae is not None else 'no decode'}",
+                               f"{f'+ KL-f8 decode {8 * zshape[-1]}x{8 * zshape[-1]}' if ae is not None else 'no decode'}",
                    "model": MODEL_NAMES.get(args.config, args.config), "per_gpu_batch": B, "global_batch": world * B,
                    "nfe": sampler.nfe, "hip_graph": not args.no_graph, "parallelism": f"dp{world} (batch-sharded)"},
         "roofline": roof,
@@ -191,16 +194,24 @@ def measured_traffic():
     return (fam["hbm_bytes_per_launch"] if fam else None), os.path.basename(files[-1])
 
 
-def gemm_roofline(prof, ncfg, rows):
+def gemm_roofline(prof, ncfg, rows, precision="bf16"):
     times_ms, flops = prof.read()
     n = len(times_ms)
     tot_t = sum(times_ms) / 1e3
     tot_f = sum(flops)
     achieved = tot_f / tot_t
-    traffic, tsrc = measured_traffic()
-    return {"bound": "mfma", "kernel": "bf16 GEMM family (all U-ViT linear layers: qkv, proj, fc1, fc2, skip_linear)",
-            "achieved": round(achieved / 1e12, 1), "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16, 4), "traffic": traffic,
+    traffic, tsrc = measured_traffic() if precision == "bf16" else (None, None)
+    kernel = "bf16 GEMM family (all U-ViT linear layers: qkv, proj, fc1, fc2, skip_linear)"
+    peak = PEAK_BF16
+    if precision == "fp8":
+        # mixed family: MXFP8 qkv/proj/fc1/fc2, bf16 skip_linear (K = 2D); peak = the FLOP-weighted harmonic mean
+        D, L = ncfg["embed_dim"], (ncfg["img_size"] // ncfg["patch_size"]) ** 2 + 2
+        f_skip = (ncfg["depth"] // 2) * 2.0 * rows * L * D * 2 * D
+        peak = tot_f / ((tot_f - f_skip) / PEAK_FP8 + f_skip / PEAK_BF16)
+        kernel = "GEMM family: MXFP8 qkv/proj/fc1/fc2 + bf16 skip_linear (FLOP-weighted fp8/bf16 peak)"
+    return {"bound": "mfma", "kernel": kernel,
+            "achieved": round(achieved / 1e12, 1), "peak": round(peak / 1e12, 1), "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic,
             "traffic_source": tsrc,
             "measured": "HIP events on the launch stream around each GEMM of the last CFG forward of the last timed step",
             "launches_per_forward": n, "avg_launch_ms": round(tot_t / n * 1e3, 4),

@@ -28,6 +28,8 @@ extern "C" {
 
 #define PDM_F32 0
 #define PDM_BF16 1
+#define PDM_FP8 2     /* OCP e4m3 bytes (MXFP8 data) */
+#define PDM_E8M0 3    /* MXFP8 block-scale dwords: [K/128][rows], byte j of (kt, r) = exponent of block kt*4 + j */
 
 /* GEMM epilogues */
 #define PDM_EPI_BF16 0   /* out_bf16 = A W^T + b */
@@ -61,6 +63,12 @@ typedef struct pdm_uvit_cfg {
   int t2i;
   int clip_dim, num_clip_token;
   int separate, enable_panoptic, num_panoptic_class;
+  /* 1: MXFP8 block linears (BASELINE configs[4] "fp8 MFMA"; class-conditional / unconditional U-ViT only,
+   * embed_dim and mlp hidden multiples of 128).  attn.qkv / attn.proj / mlp.fc1 / mlp.fc2 weights are then
+   * PDM_FP8 [out][in] with a "<key>_scale" PDM_E8M0 [in/128][out] companion (qkv / fc1: quantised after the
+   * norm fold); every activation feeding them is MXFP8, written by the epilogue that produces it.  Everything
+   * else (skip_linear, whose output replaces the residual stream, attention, heads) stays as in the bf16 path. */
+  int fp8;
 } pdm_uvit_cfg;
 
 /* replaces utils.get_nnet (utils.py:291-299) + UViT.__init__ (libs/uvit.py:139-195) */
@@ -178,6 +186,12 @@ int pdm_attention(const void* qkv, int ldq, void* out, int ldo, int B, int L, in
                   void* stream);
 /* fp32 -> bf16 conversion */
 int pdm_f32_to_bf16(const float* x, void* y, long long n, void* stream);
+/* MXFP8 quantisation of rows x [rows][ldx] (dtype PDM_F32 or PDM_BF16, K % 32 == 0) -> e4m3 q [rows][ldq] and
+ * E8M0 scale dwords s [ceil(K/128)][s_ld >= rows]: exponent ceil(log2(amax/448)) per 32 columns, RNE data (the
+ * quantiser of every MXFP8-emitting epilogue; in the fp8 forward it turns the attention output into the
+ * attn.proj operand) */
+int pdm_mx_quantize(const void* x, int dtype, int ldx, int rows, int K, void* q, int ldq, unsigned* s, int s_ld,
+                    void* stream);
 
 /* ---------------------------------------------------------------------------------------------------
  * KL-f8 decoder: FrozenAutoencoderKL.decode (libs/autoencoder.py:446-450) = z / scale_factor ->

@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpdm.so")
 
-PDM_F32, PDM_BF16 = 0, 1
+PDM_F32, PDM_BF16, PDM_FP8, PDM_E8M0 = 0, 1, 2, 3
 EPI_BF16, EPI_GELU, EPI_F32 = 0, 1, 2
 
 
@@ -20,7 +20,7 @@ class PdmUvitCfg(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "img_size", "patch_size", "in_chans", "embed_dim", "depth", "num_heads", "mlp_hidden", "num_classes",
         "conv", "skip", "qkv_bias", "mlp_time_embed", "t2i", "clip_dim", "num_clip_token", "separate",
-        "enable_panoptic", "num_panoptic_class")]
+        "enable_panoptic", "num_panoptic_class", "fp8")]
 
 
 class PdmDecoderCfg(ctypes.Structure):
@@ -109,6 +109,8 @@ _SIGS = {
     "pdm_attention": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p]),
     "pdm_f32_to_bf16": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]),
+    "pdm_mx_quantize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "pdm_images_to_u8": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_void_p]),
     "pdm_mask_bits_to_rgb": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -227,7 +229,7 @@ def gemm_ln(a, w, bias, epi, ln_stats=None, ln_colsum=None, out=None, out_f32=No
 # ---- MXFP8 (OCP e4m3 + E8M0 per 32 elements) host reference and GEMM wrapper --------------------------
 
 def mx_quantize(x):
-    """MXFP8 of x [R, K] (K % 128 == 0) exactly as the GPU epilogue quantises (csrc/pdm_common.h mx_quant8):
+    """MXFP8 of x [R, K] (K % 32 == 0) exactly as the GPU epilogue quantises (csrc/pdm_common.h mx_quant8):
     E8M0 exponent e = ceil(log2(amax/448)) + 127 per 32 consecutive elements, e4m3 = RNE(x * 2^(127 - e)).
     Returns (q [R, K] float8_e4m3fn, scale dwords [K/128, R] int32: byte j of (kt, r) = block kt*4 + j)."""
     R, K = x.shape
@@ -238,7 +240,10 @@ def mx_quantize(x):
     e = e.clamp(max=254)
     inv = ((254 - e) << 23).view(torch.float32)
     q = (xb * inv[..., None]).reshape(R, K).to(torch.float8_e4m3fn)
-    sc = e.to(torch.uint8).reshape(R, K // 128, 4).permute(1, 0, 2).contiguous().view(torch.int32).reshape(K // 128, R)
+    kt = (K + 127) // 128   # K % 128 != 0: the last scale dword is zero-padded
+    e8 = torch.zeros(R, kt * 4, dtype=torch.uint8, device=x.device)
+    e8[:, : K // 32] = e.to(torch.uint8)
+    sc = e8.reshape(R, kt, 4).permute(1, 0, 2).contiguous().view(torch.int32).reshape(kt, R)
     return q, sc
 
 
@@ -247,6 +252,20 @@ def mx_dequantize(q, sc):
     e = sc.contiguous().view(torch.uint8).reshape(K // 128, R, 4).permute(1, 0, 2).reshape(R, K // 32).to(torch.int32)
     scale = torch.pow(2.0, (e - 127).double()).float()
     return (q.float().reshape(R, K // 32, 32) * scale[..., None]).reshape(R, K)
+
+
+def mx_quantize_gpu(x):
+    """MXFP8 of fp32 / bf16 rows x [R, K] on the GPU (pdm_mx_quantize): (q float8_e4m3fn [R, K], scale dwords
+    int32 [ceil(K/128), R]), bit-identical to mx_quantize."""
+    lib = load()
+    require_gpu(x)
+    R, K = x.shape
+    q = torch.empty(R, K, dtype=torch.float8_e4m3fn, device=x.device)
+    s = torch.zeros((K + 127) // 128, R, dtype=torch.int32, device=x.device)
+    dt = PDM_F32 if x.dtype == torch.float32 else PDM_BF16
+    check(lib.pdm_mx_quantize(ptr(x), dt, x.stride(0), R, K, ptr(q), q.stride(0), ptr(s), R, stream_ptr(x.device)),
+          "pdm_mx_quantize")
+    return q, s
 
 
 def gemm_ex(epi, a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=None, accumulate=False,

@@ -39,6 +39,7 @@ CONFIGS = {
                   use_checkpoint=True, conv=False),
         z_shape=(4, 64, 64), front_end="dpm_solver_pp", cfg_scale=0.7, decode=True,
         scale_factor=0.18215, sample_steps=50, mini_batch_size=50,
+        precision="fp8",   # BASELINE configs[4]: "fp8 MFMA attention/MLP" (UViT.set_precision)
     ),
     "mscoco_uvit_small": dict(
         nnet=dict(name="uvit_t2i", img_size=32, in_chans=4, patch_size=2, embed_dim=512, depth=12,

@@ -80,19 +80,28 @@ struct pdm_uvit {
   // norm1 / norm2 are folded into the next Linear (fused LayerNorm, see GemmArgs): the registered
   // attn.qkv.weight / mlp.fc1.weight are W * diag(norm.weight) in bf16, ln_colsum their row sums and ln_bias
   // W norm.bias (+ the Linear's own bias), both fp32 (include/pdm.h)
+  // a block Linear's weight [N][K]: bf16, or (cfg.fp8) e4m3 bytes + "<key>_scale" E8M0 dwords [K/128][N]
+  void add_lin(const std::string& key, long long N, long long K) {
+    if (cfg.fp8) {
+      add(key, PDM_FP8, N * K);
+      add(key + "_scale", PDM_E8M0, K / 128 * N);
+    } else {
+      add(key, PDM_BF16, N * K);
+    }
+  }
   void add_block(const std::string& pre, bool skip) {
-    add(pre + ".attn.qkv.weight", PDM_BF16, 3LL * D * D);
+    add_lin(pre + ".attn.qkv.weight", 3LL * D, D);
     add(pre + ".attn.qkv.ln_colsum", PDM_F32, 3LL * D);
     add(pre + ".attn.qkv.ln_bias", PDM_F32, 3LL * D);
-    add(pre + ".attn.proj.weight", PDM_BF16, 1LL * D * D);
+    add_lin(pre + ".attn.proj.weight", D, D);
     add(pre + ".attn.proj.bias", PDM_F32, D);
-    add(pre + ".mlp.fc1.weight", PDM_BF16, 1LL * Hid * D);
+    add_lin(pre + ".mlp.fc1.weight", Hid, D);
     add(pre + ".mlp.fc1.ln_colsum", PDM_F32, Hid);
     add(pre + ".mlp.fc1.ln_bias", PDM_F32, Hid);
-    add(pre + ".mlp.fc2.weight", PDM_BF16, 1LL * D * Hid);
+    add_lin(pre + ".mlp.fc2.weight", D, Hid);
     add(pre + ".mlp.fc2.bias", PDM_F32, D);
     if (skip) {
-      add(pre + ".skip_linear.weight", PDM_BF16, 2LL * D * D);
+      add(pre + ".skip_linear.weight", PDM_BF16, 2LL * D * D);   // bf16 in both modes (run_block8)
       add(pre + ".skip_linear.bias", PDM_F32, D);
     }
   }
@@ -101,6 +110,16 @@ struct pdm_uvit {
 namespace {
 
 // ------------------------------------------------------------------------------------------------
+// An MXFP8 matrix in the GemmArgs operand layout: e4m3 rows q [rows][ld] (bytes) and E8M0 scale dwords
+// s [K/128][sld].  cols(k0) is the same rows from column k0 on (k0 % 128 == 0).
+struct Q8 {
+  unsigned char* q = nullptr;
+  int ld = 0;
+  unsigned* s = nullptr;
+  int sld = 0;
+  Q8 cols(int k0) const { return Q8{q + k0, ld, s + (size_t)(k0 / 128) * sld, sld}; }
+};
+
 // workspace layout
 struct Workspace {
   float* X;     // [rows*Lx, D] residual stream (image)
@@ -121,6 +140,11 @@ struct Workspace {
   bf16* MXIN;   // [rows*Lm, D] bf16 copy of the mask-stream block input (qkv / skip_linear operand)
   bf16* SKM;    // [nhalf][rows*Lm, D]
   float* STM;   // [rows*Lm, T] LayerNorm partials of the mask stream
+  // fp8 forward (cfg.fp8): MXFP8 operands of the block Linears, e4m3 rows + E8M0 scale dwords [K/128][rows*Lx]
+  Q8 xq;             // block input x (from the token assembly row pass)                 [rows*Lx, D]
+  Q8 xtq;            // block-internal x (skip_linear / proj epilogues: qkv / fc1 operand) [rows*Lx, D]
+  Q8 atq;            // attention output (proj operand)                                  [rows*Lx, D]
+  Q8 mlq;            // GELU(fc1) (fc2 operand)                                          [rows*Lx, Hid]
   size_t bytes;
 };
 
@@ -138,16 +162,31 @@ Workspace layout(const pdm_uvit* h, int rows, char* base) {
   const size_t Mm = mask ? (size_t)rows * h->Lm : 0;
   const size_t Mmax = Mx > Mm ? Mx : Mm;
   const size_t T = (D + 255) / 256;
+  const bool f8 = h->cfg.fp8 != 0;   // MXFP8 operands replace XT / MLP; XB / SK stay (bf16 skip_linear)
   w.X = (float*)take(Mx * D * 4);
   w.XB = (bf16*)take(Mx * D * 2);
-  w.XT = (bf16*)take(Mmax * D * 2);
+  if (!f8) w.XT = (bf16*)take(Mmax * D * 2);
   w.ST = (float*)take(Mmax * T * 8);
   w.STT = (float*)take(Mmax * T * 8);
   w.QKV = (bf16*)take(Mmax * 3 * D * 2);
   w.ATT = (bf16*)take(Mmax * D * 2);
-  w.MLP = (bf16*)take(Mmax * h->Hid * 2);
+  if (!f8) w.MLP = (bf16*)take(Mmax * h->Hid * 2);
   w.SK = (bf16*)take((size_t)h->nhalf * Mx * D * 2);
   w.HEADIN = (bf16*)take((size_t)rows * h->n_patch * D * 2);
+  if (f8) {
+    auto q8 = [&](size_t K) {
+      Q8 r;
+      r.q = (unsigned char*)take(Mx * K);
+      r.ld = (int)K;
+      r.s = (unsigned*)take(K / 128 * Mx * 4);
+      r.sld = (int)Mx;
+      return r;
+    };
+    w.xq = q8(D);
+    w.xtq = q8(D);
+    w.atq = q8(D);
+    w.mlq = q8(h->Hid);
+  }
   if (h->cfg.t2i) {
     w.CTXF = (float*)take((size_t)rows * h->cfg.num_clip_token * D * 4);
     w.CTXB = (bf16*)take((size_t)rows * h->cfg.num_clip_token * h->cfg.clip_dim * 2);
@@ -176,6 +215,21 @@ struct LnIO {
   const float* colsum = nullptr;
 };
 
+// checked launch + the profiling hook (HIP events around every GEMM of the forward)
+int launch_gemm(const Ctx& c, const pdm::GemmArgs& a, int epi) {
+  PDM_CHECK(pdm::gemm_check(a, epi));
+  const pdm_uvit* h = c.h;
+  const bool prof = h->prof_on && 2 * (h->prof_n + 1) <= (int)h->prof_ev.size();
+  if (prof) PDM_HIP(hipEventRecord(h->prof_ev[2 * h->prof_n], c.s));
+  PDM_HIP(pdm::gemm_launch(a, epi, c.s));
+  if (prof) {
+    PDM_HIP(hipEventRecord(h->prof_ev[2 * h->prof_n + 1], c.s));
+    h->prof_flops[h->prof_n] = 2.0 * a.M * a.N * a.K;
+    ++h->prof_n;
+  }
+  return PDM_OK;
+}
+
 int gemm(const Ctx& c, const bf16* A, int lda, const bf16* W, const float* bias, int M, int N, int K, int epi,
          bf16* ob, int ldo, float* of, int ldr, int accumulate, const bf16* A2 = nullptr, int lda2 = 0, int K1 = 0,
          int a_rpg = 0, int a_gs = 0, LnIO ln = LnIO()) {
@@ -192,17 +246,28 @@ int gemm(const Ctx& c, const bf16* A, int lda, const bf16* W, const float* bias,
   a.out_f32 = of; a.ldr = ldr;
   a.accumulate = accumulate;
   a.a_rows_per_group = a_rpg; a.a_group_stride = a_gs;
-  PDM_CHECK(pdm::gemm_check(a, epi));
+  return launch_gemm(c, a, epi);
+}
+
+// MXFP8 block Linear (cfg.fp8): A and the weight `wkey` (+ "<wkey>_scale") on the block-scaled MFMA; the
+// epilogue also writes the MXFP8 copy of what it stores into `out` when out.q is set (the next Linear's operand)
+int gemm8(const Ctx& c, const Q8& A, const std::string& wkey, const float* bias, int M, int N, int K, int epi,
+          bf16* ob, float* of, int accumulate, LnIO ln, const Q8& out) {
   const pdm_uvit* h = c.h;
-  const bool prof = h->prof_on && 2 * (h->prof_n + 1) <= (int)h->prof_ev.size();
-  if (prof) PDM_HIP(hipEventRecord(h->prof_ev[2 * h->prof_n], c.s));
-  PDM_HIP(pdm::gemm_launch(a, epi, c.s));
-  if (prof) {
-    PDM_HIP(hipEventRecord(h->prof_ev[2 * h->prof_n + 1], c.s));
-    h->prof_flops[h->prof_n] = 2.0 * M * N * K;
-    ++h->prof_n;
-  }
-  return PDM_OK;
+  pdm::GemmArgs a{};
+  const int T = (h->D + 255) / 256;
+  a.stats_out = ln.st_out; a.stats_ld = T;
+  a.ln_stats = ln.st_in; a.ln_ld = T; a.ln_D = K; a.ln_eps = 1e-5f; a.ln_colsum = ln.colsum;
+  a.A1 = (const bf16*)A.q; a.lda1 = A.ld; a.K1 = K;
+  a.W = (const bf16*)h->ptr(wkey); a.bias = bias;
+  a.M = M; a.N = N; a.K = K;
+  a.out_bf16 = ob; a.ldo = ob ? N : 0;
+  a.out_f32 = of; a.ldr = of ? h->D : 0; a.accumulate = accumulate;
+  a.fp8 = 1;
+  a.a_scale = A.s; a.a_scale_ld = A.sld;
+  a.w_scale = (const unsigned*)h->ptr(wkey + "_scale"); a.w_scale_ld = N;
+  a.out_fp8 = out.q; a.ldo8 = out.ld; a.out_scale = out.s; a.out_scale_ld = out.sld;
+  return launch_gemm(c, a, epi);
 }
 
 #define PDM_TRY(x)           \
@@ -296,6 +361,96 @@ int run_stack(const Ctx& c, const Workspace& w, int rows, int L) {
   return PDM_OK;
 }
 
+// One U-ViT Block with MXFP8 qkv / proj / fc1 / fc2 (cfg.fp8, BASELINE configs[4]).  `in` is the MXFP8 block
+// input x with LayerNorm partials st_in.  Out-blocks with a long skip start from skip_linear(cat([x, skip]))
+// (libs/uvit.py:116-117) instead, kept in bf16 on the split-K GEMM over xb_in / skip_in: its output REPLACES the
+// residual stream, and in MXFP8 it alone costs 6.3e-2 rel-L2 of the H/4 forward (vs 1.6-4.4e-2 for each of the
+// other Linears; fp32 fake-quant of the oracle) for 7 % of the FLOPs.  Attention stays bf16 (a
+// 72-deep QK^T cannot fill the 128-deep scaled MFMA, and the unscaled fp8 MFMA runs at the bf16 rate); its output
+// is MX-quantised for proj.  fc2 leaves the block output as MXFP8 in out8 and / or bf16 in outb (either may be
+// null) and its partials in st_out.
+int run_block8(const Ctx& c, const std::string& pre, float* X, int M, int L, const Q8& in, const float* st_in,
+               const bf16* xb_in, const bf16* skip_in, const Q8& out8, bf16* outb, float* st_out, const Workspace& w) {
+  const pdm_uvit* h = c.h;
+  const int D = h->D;
+  Q8 a = in;
+  const float* st = st_in;
+  if (skip_in) {  // x = skip_linear(cat([x, skip], -1)) -> X (fp32) + its MXFP8 copy (qkv operand) + partials
+    pdm::GemmArgs g{};
+    g.A1 = xb_in; g.lda1 = D; g.A2 = skip_in; g.lda2 = D; g.K1 = D;
+    g.W = h->w(pre + ".skip_linear.weight"); g.bias = h->f(pre + ".skip_linear.bias");
+    g.M = M; g.N = D; g.K = 2 * D;
+    g.out_f32 = X; g.ldr = D;
+    g.stats_out = w.STT; g.stats_ld = (D + 255) / 256;
+    g.out_fp8 = w.xtq.q; g.ldo8 = w.xtq.ld; g.out_scale = w.xtq.s; g.out_scale_ld = w.xtq.sld;
+    PDM_TRY(launch_gemm(c, g, pdm::EPI_F32));
+    a = w.xtq;
+    st = w.STT;
+  }
+  {  // qkv = norm1(x) W^T (bf16 for the attention kernel)
+    LnIO io;
+    io.st_in = st;
+    io.colsum = h->f(pre + ".attn.qkv.ln_colsum");
+    PDM_TRY(gemm8(c, a, pre + ".attn.qkv.weight", h->f(pre + ".attn.qkv.ln_bias"), M, 3 * D, D, pdm::EPI_BF16, w.QKV,
+                  nullptr, 0, io, Q8()));
+  }
+  {
+    pdm::AttentionArgs at{};
+    at.qkv = w.QKV; at.ldq = 3 * D;
+    at.out = w.ATT; at.ldo = D;
+    at.B = M / L; at.L = L; at.H = h->H; at.Dh = h->Dh;
+    at.scale = 1.0f / sqrtf((float)h->Dh);
+    PDM_CHECK(pdm::attention_check(at));
+    PDM_HIP(pdm::attention_launch(at, c.s));
+    PDM_HIP(pdm::mxq_launch(w.ATT, 1, D, M, D, w.atq.q, w.atq.ld, w.atq.s, w.atq.sld, c.s));
+  }
+  {  // x += proj(attn)
+    LnIO io;
+    io.st_out = w.STT;
+    PDM_TRY(gemm8(c, w.atq, pre + ".attn.proj.weight", h->f(pre + ".attn.proj.bias"), M, D, D, pdm::EPI_F32, nullptr,
+                  X, 1, io, w.xtq));
+  }
+  {  // h = GELU(fc1(norm2(x))), stored only as the MXFP8 fc2 operand
+    LnIO io;
+    io.st_in = w.STT;
+    io.colsum = h->f(pre + ".mlp.fc1.ln_colsum");
+    PDM_TRY(gemm8(c, w.xtq, pre + ".mlp.fc1.weight", h->f(pre + ".mlp.fc1.ln_bias"), M, h->Hid, D, pdm::EPI_GELU,
+                  nullptr, nullptr, 0, io, w.mlq));
+  }
+  {  // x += fc2(h)
+    LnIO io;
+    io.st_out = st_out;
+    PDM_TRY(gemm8(c, w.mlq, pre + ".mlp.fc2.weight", h->f(pre + ".mlp.fc2.bias"), M, D, h->Hid, pdm::EPI_F32, outb,
+                  X, 1, io, out8));
+  }
+  return PDM_OK;
+}
+
+// The block stack with MXFP8 block Linears: in-blocks leave their output as MXFP8 (the next block's operand) and
+// as bf16 in SK[i] (the long skip); the mid block and out-blocks leave bf16 x in XB for the next skip_linear (or,
+// without long skips, MXFP8 x for the next qkv).  Every activation is produced once, by the epilogue that computes
+// it, in the precision and layout of its consumer.
+int run_stack8(const Ctx& c, const Workspace& w, int rows, int L) {
+  const pdm_uvit* h = c.h;
+  const int D = h->D, M = rows * L, n = h->nhalf;
+  const bool skip = h->cfg.skip != 0;
+  const size_t MD = (size_t)M * D;
+  PDM_HIP(pdm::rowstats_launch(w.X, D, M, D, nullptr, 0, w.ST, (D + 255) / 256, c.s, w.xq.q, w.xq.ld, w.xq.s,
+                               w.xq.sld));
+  for (int i = 0; i < n; ++i)
+    PDM_TRY(run_block8(c, "in_blocks." + std::to_string(i), w.X, M, L, w.xq, w.ST, nullptr, nullptr, w.xq,
+                       skip ? w.SK + i * MD : nullptr, w.ST, w));
+  PDM_TRY(run_block8(c, "mid_block", w.X, M, L, w.xq, w.ST, nullptr, nullptr, skip ? Q8() : w.xq,
+                     skip ? w.XB : nullptr, w.ST, w));
+  for (int i = 0; i < n; ++i) {
+    const bool last = i + 1 == n;
+    PDM_TRY(run_block8(c, "out_blocks." + std::to_string(i), w.X, M, L, w.xq, w.ST, w.XB,
+                       skip ? w.SK + (n - 1 - i) * MD : nullptr, last || skip ? Q8() : w.xq,
+                       last || !skip ? nullptr : w.XB, last ? nullptr : w.ST, w));
+  }
+  return PDM_OK;
+}
+
 int check_ready(pdm_uvit* h) {
   for (auto& n : h->order)
     if (!h->params[n].ptr) return fail(PDM_ERR_STATE, "pdm_uvit: weight not registered: " + n);
@@ -382,6 +537,9 @@ int pdm_uvit_create(const pdm_uvit_cfg* cfg, pdm_uvit** out) {
   if (c.mlp_hidden % 64) return fail(PDM_ERR_ARG, "mlp hidden size must be a multiple of 64");
   if (c.t2i && c.enable_panoptic && !c.separate)
     return fail(PDM_ERR_ARG, "uvit_t2i with enable_panoptic and separate=False is not supported by the HIP path");
+  if (c.fp8 && c.t2i) return fail(PDM_ERR_ARG, "fp8: only the class-conditional / unconditional U-ViT has an MXFP8 path");
+  if (c.fp8 && (c.embed_dim % 128 || c.mlp_hidden % 128))
+    return fail(PDM_ERR_ARG, "fp8: embed_dim and the mlp hidden size must be multiples of 128 (MXFP8 K-tiles)");
   pdm_uvit* h = new pdm_uvit();
   h->cfg = c;
   h->D = c.embed_dim;
@@ -546,7 +704,7 @@ int pdm_uvit_forward(pdm_uvit* h, const float* x, const float* t, const int64_t*
     PDM_CHECK(pdm::assemble_check(a));
     PDM_HIP(pdm::assemble_launch(a, c.s));
   }
-  PDM_TRY(run_stack(c, w, rows, L));
+  PDM_TRY(h->cfg.fp8 ? run_stack8(c, w, rows, L) : run_stack(c, w, rows, L));
   PDM_TRY(final_norm(c, w, rows, w.X, L));
   PDM_TRY(run_head(c, w.HEADIN, h->n_patch, 0, rows, "decoder_pred", h->C, h->P, h->P_pad, eps_pre));
   return PDM_OK;
@@ -792,6 +950,17 @@ int pdm_attention(const void* qkv, int ldq, void* out, int ldo, int B, int L, in
   a.B = B; a.L = L; a.H = H; a.Dh = Dh; a.scale = scale;
   PDM_CHECK(pdm::attention_check(a));
   PDM_HIP(pdm::attention_launch(a, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_mx_quantize(const void* x, int dtype, int ldx, int rows, int K, void* q, int ldq, unsigned* s, int s_ld,
+                    void* stream) {
+  if (dtype != PDM_F32 && dtype != PDM_BF16) return fail(PDM_ERR_ARG, "pdm_mx_quantize: dtype must be PDM_F32 or PDM_BF16");
+  const hipError_t e = pdm::mxq_launch(x, dtype == PDM_F32 ? 0 : 1, ldx, rows, K, (unsigned char*)q, ldq, s, s_ld,
+                                       (hipStream_t)stream);
+  if (e == hipErrorInvalidValue)
+    return fail(PDM_ERR_ARG, "pdm_mx_quantize: K % 32, ldx / ldq >= K, s_ld >= rows and 16-byte aligned rows required");
+  PDM_HIP(e);
   return PDM_OK;
 }
 

@@ -1262,7 +1262,8 @@ const char* gemm_check(const GemmArgs& p, int epi) {
       return "gemm: fused LayerNorm needs ln_colsum and ln_ld = ceil(ln_D / 256)";
   }
   if (epi == EPI_BF16 || epi == EPI_GELU) {
-    if (!p.out_bf16 || (p.ldo % 4)) return "gemm: bf16 output missing or ldo not a multiple of 4";
+    // the MXFP8 copy alone is a valid output (fc1 -> fc2 operand of the fp8 forward)
+    if ((!p.out_bf16 && !p.out_fp8) || (p.out_bf16 && p.ldo % 4)) return "gemm: bf16 output missing or ldo not a multiple of 4";
   } else if (epi == EPI_F32) {
     if (!p.out_f32 || (p.ldr % 4)) return "gemm: f32 output missing or ldr not a multiple of 4";
     if (p.out_bf16 && (p.ldo % 4)) return "gemm: ldo not a multiple of 4";

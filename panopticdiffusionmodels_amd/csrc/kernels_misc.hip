@@ -65,7 +65,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs p) {
 // covers columns 256 i .. 256 i + 255, i.e. exactly one partial group, so each group is two wave sums.
 template <int NV>
 __global__ __launch_bounds__(256) void rowstats_kernel(const float* x, int ldx, int rows, int D, bf16* xb, int ldb,
-                                                       float* stats, int stats_ld) {
+                                                       float* stats, int stats_ld, unsigned char* xq, int ldq,
+                                                       unsigned* xs, int xs_ld) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + wave;
   if (r >= rows) return;
@@ -78,6 +79,15 @@ __global__ __launch_bounds__(256) void rowstats_kernel(const float* x, int ldx, 
     const bool ok = idx < nv;
     const f32x4 v = ok ? xr[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
     if (ok && xb) *reinterpret_cast<bf16x4*>(xb + (size_t)r * ldb + 4 * idx) = to_bf16x4(v[0], v[1], v[2], v[3]);
+    if (xq) {   // MXFP8 copy: 8 consecutive lanes hold one 32-column block
+      unsigned e8;
+      const unsigned q = mx_quant4(v, &e8);
+      if (ok) {
+        *reinterpret_cast<unsigned*>(xq + (size_t)r * ldq + 4 * idx) = q;
+        if ((lane & 7) == 0)
+          reinterpret_cast<unsigned char*>(xs)[((size_t)(idx >> 5) * xs_ld + r) * 4 + ((idx >> 3) & 3)] = (unsigned char)e8;
+      }
+    }
     const float s = wave_sum((v[0] + v[1]) + (v[2] + v[3]));
     const float mu = s / (float)min(256, D - 256 * i);
     const f32x4 d = v - mu;
@@ -321,6 +331,39 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* x, bf16* y,
   for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) y[e] = (bf16)x[e];
 }
 
+// ------------------------------------------------------------------------------------------------
+// MXFP8 quantisation of rows (pdm_mx_quantize; in the fp8 forward: attention output -> attn.proj operand).
+// One thread per 8 consecutive columns, so the 4 consecutive lanes of a 32-column block reduce its amax with
+// two xor-shuffles (mx_quant8: the quantiser of the MXFP8-emitting GEMM epilogues, bit for bit).
+template <typename T>
+__global__ __launch_bounds__(256) void mxq_kernel(const T* x, int ldx, int rows, int K, unsigned char* q, int ldq,
+                                                  unsigned* s, int s_ld) {
+  const int nch = K >> 3;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const bool ok = i < (long long)rows * nch;
+  const int r = ok ? (int)(i / nch) : 0;
+  const int c = ok ? (int)(i - (long long)r * nch) : 0;
+  float f[8];
+  if (ok) {
+    const T* p = x + (size_t)r * ldx + c * 8;
+    if constexpr (sizeof(T) == 4) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { f[j] = a[j]; f[4 + j] = b[j]; }
+    } else {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = 0.f;
+  }
+  unsigned e8;
+  const uint2 w = mx_quant8(f, &e8);   // every lane joins the block shuffles (K % 32 == 0: blocks never straddle rows)
+  if (ok) mx_store8(q, ldq, s, s_ld, r, c * 8, w, e8, (c & 3) == 0);
+}
+
 inline int grid_for(long long n) {
   long long g = (n + 255) / 256;
   if (g > 8192) g = 8192;
@@ -354,12 +397,13 @@ hipError_t layernorm_launch(const LayerNormArgs& p, hipStream_t stream) {
 }
 
 hipError_t rowstats_launch(const float* x, int ldx, int rows, int D, bf16* xb, int ldb, float* stats, int stats_ld,
-                           hipStream_t stream) {
+                           hipStream_t stream, unsigned char* xq, int ldq, unsigned* xs, int xs_ld) {
   if (!x || !stats || rows <= 0 || D <= 0 || D % 4 || D > 2048 || stats_ld < (D + 255) / 256 || ldx % 4 ||
-      (xb && ldb % 4))
+      (xb && ldb % 4) || (xq && (D % 32 || ldq % 4 || !xs || xs_ld < rows)))
     return hipErrorInvalidValue;
   dim3 grid((rows + 3) / 4), block(256);
-  hipLaunchKernelGGL(rowstats_kernel<8>, grid, block, 0, stream, x, ldx, rows, D, xb, ldb, stats, stats_ld);
+  hipLaunchKernelGGL(rowstats_kernel<8>, grid, block, 0, stream, x, ldx, rows, D, xb, ldb, stats, stats_ld, xq, ldq,
+                     xs, xs_ld);
   return hipGetLastError();
 }
 
@@ -424,6 +468,20 @@ hipError_t lincomb_launch(float* out, int n_terms, const float* const* T, const 
 
 hipError_t cast_bf16_launch(const float* x, bf16* y, long long n, hipStream_t stream) {
   hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, stream, x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t mxq_launch(const void* x, int dtype, int ldx, int rows, int K, unsigned char* q, int ldq, unsigned* s,
+                      int s_ld, hipStream_t stream) {
+  const bool f32 = dtype == 0;
+  if (!x || !q || !s || rows <= 0 || K <= 0 || K % 32 || ldx < K || ldq < K || ldq % 8 || s_ld < rows ||
+      (dtype != 0 && dtype != 1) || (f32 ? ldx % 4 : ldx % 8) || ((uintptr_t)x & 15) || ((uintptr_t)q & 7) ||
+      ((uintptr_t)s & 3))
+    return hipErrorInvalidValue;
+  const long long n = (long long)rows * (K >> 3);
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  if (f32) hipLaunchKernelGGL(mxq_kernel<float>, grid, block, 0, stream, (const float*)x, ldx, rows, K, q, ldq, s, s_ld);
+  else hipLaunchKernelGGL(mxq_kernel<bf16>, grid, block, 0, stream, (const bf16*)x, ldx, rows, K, q, ldq, s, s_ld);
   return hipGetLastError();
 }
 

@@ -95,6 +95,24 @@ __device__ __forceinline__ uint2 mx_quant8(const float (&v)[8], unsigned* e8) {
   return make_uint2((unsigned)w0, (unsigned)w1);
 }
 
+// the same for a block spread over 8 consecutive lanes with 4 values each (row kernels, float4 per lane)
+__device__ __forceinline__ unsigned mx_quant4(const f32x4& v, unsigned* e8) {
+  float am = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  am = fmaxf(am, __shfl_xor(am, 4, 64));
+  const unsigned bits = __float_as_uint(am * (1.0f / 448.0f));
+  unsigned e = (bits >> 23) & 0xffu;
+  e += (bits & 0x7fffffu) ? 1u : 0u;
+  e = e > 254u ? 254u : e;
+  const float inv = __uint_as_float((254u - e) << 23);
+  int w = 0;
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, w, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, w, true);
+  *e8 = e;
+  return (unsigned)w;
+}
+
 // store of one quantised 8-column piece (row m, columns n .. n+7) of an MXFP8 output, and of its block scale
 // by the block's first lane
 __device__ __forceinline__ void mx_store8(unsigned char* out, int ldo8, unsigned* scale, int scale_ld, int m, int n,

@@ -58,10 +58,11 @@ struct GemmArgs {
 void gemm_set_tuning(int raster, int dbg_tile0);
 
 // Row partials of the fused LayerNorm: X fp32 [rows, D] -> stats [rows, ceil(D/256)] (sum, M2) per 256-column
-// group (+ optional bf16 copy xb [rows, D]).  Used where no GEMM epilogue produced them (token assembly, the
+// group (+ optional bf16 copy xb [rows, D], + optional MXFP8 copy xq / xs in the GemmArgs A-operand layout).  Used where no GEMM epilogue produced them (token assembly, the
 // t2i mask-stream refresh, and behind the 128-tile GEMM policy).
 hipError_t rowstats_launch(const float* x, int ldx, int rows, int D, bf16* xb, int ldb, float* stats, int stats_ld,
-                           hipStream_t stream);
+                           hipStream_t stream, unsigned char* xq = nullptr, int ldq = 0, unsigned* xs = nullptr,
+                           int xs_ld = 0);
 
 const char* gemm_check(const GemmArgs& p, int epi);
 hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream);
@@ -156,6 +157,11 @@ hipError_t epilogue_launch(const EpilogueArgs& p, hipStream_t stream);
 int set_error(int code, const std::string& msg);
 
 hipError_t cast_bf16_launch(const float* x, bf16* y, long long n, hipStream_t stream);
+
+// MXFP8 copy of fp32 (dtype 0) / bf16 (dtype 1) rows x [rows][ldx] -> e4m3 q [rows][ldq] + E8M0 scale dwords
+// s [K/128][s_ld] (GemmArgs A-operand layout); hipErrorInvalidValue on a bad shape / stride / alignment
+hipError_t mxq_launch(const void* x, int dtype, int ldx, int rows, int K, unsigned char* q, int ldq, unsigned* s,
+                      int s_ld, hipStream_t stream);
 
 // out = sum_i c_i * T_i over n elements (fp32); used by the generic solver path.
 hipError_t lincomb_launch(float* out, int n_terms, const float* const* T, const float* c, long long n, hipStream_t stream);

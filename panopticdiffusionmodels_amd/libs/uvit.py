@@ -77,6 +77,7 @@ class UViT(HipNet):
                  qkv_bias=False, qk_scale=None, norm_layer=nn.LayerNorm, mlp_time_embed=False, num_classes=-1,
                  use_checkpoint=False, conv=True, skip=True):
         super().__init__()
+        self.precision = "bf16"
         if qk_scale is not None:
             raise ValueError("qk_scale other than the default head_dim ** -0.5 is not supported")
         self.num_features = self.embed_dim = embed_dim
@@ -109,7 +110,17 @@ class UViT(HipNet):
         return dict(img_size=self.img_size, patch_size=self.patch_size, in_chans=self.in_chans,
                     embed_dim=self.embed_dim, depth=self.depth, num_heads=self.num_heads, mlp_ratio=self.mlp_ratio,
                     num_classes=self.num_classes, conv=self.conv, skip=self.skip, qkv_bias=self.qkv_bias,
-                    mlp_time_embed=self.mlp_time_embed)
+                    mlp_time_embed=self.mlp_time_embed, fp8=self.precision == "fp8")
+
+    def set_precision(self, precision):
+        """'bf16' (default) or 'fp8': the block Linears (qkv, proj, fc1, fc2, skip_linear) as MXFP8 GEMMs on the
+        block-scaled MFMA, every other op unchanged (BASELINE configs[4], imagenet512_uvit_huge; include/pdm.h
+        pdm_uvit_cfg.fp8).  Not a reference option: the reference computes in the autocast dtype."""
+        if precision not in ("bf16", "fp8"):
+            raise ValueError(f"precision must be 'bf16' or 'fp8', got {precision!r}")
+        self.precision = precision
+        self.invalidate()
+        return self
 
     @torch.jit.ignore
     def no_weight_decay(self):

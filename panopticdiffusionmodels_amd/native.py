@@ -4,7 +4,8 @@ The module keeps fp32 parameters under the reference's state_dict keys (so `load
 reference checkpoint works unchanged, eval_ldm_discrete.py:46).  On first GPU use the parameters are
 packed once into the layouts libpdm expects (Linear weights -> bf16 [out, in]; decoder heads padded to a
 multiple of 16 rows; conv / embedding tables fp32; norm1 / norm2 folded into attn.qkv / mlp.fc1, see
-`_ln_fold`) and their device addresses are registered with the handle.  Any load_state_dict / .to() invalidates the packed copy.
+`_ln_fold`; with fp8=True the block Linears as MXFP8, see `_mx_weight`) and their device addresses are
+registered with the handle.  Any load_state_dict / .to() invalidates the packed copy.
 """
 import ctypes
 
@@ -35,6 +36,7 @@ def cfg_struct(kw, t2i):
     c.separate = int(bool(kw.get("separate", False))) if t2i else 0
     c.enable_panoptic = int(bool(kw.get("enable_panoptic", True))) if t2i else 0
     c.num_panoptic_class = int(kw.get("num_panoptic_class", 8)) if t2i else 0
+    c.fp8 = int(bool(kw.get("fp8", False)))
     return c
 
 
@@ -50,6 +52,7 @@ class NativeHandle:
         self.cfg = cfg
         self.packed = {}
         self.ws = None
+        self._mx = {}   # MXFP8 copies of the block Linears while packing (fp8 only)
         sd = module.state_dict()
         dev = next(iter(sd.values())).device
         n = lib.pdm_uvit_param_count(h)
@@ -64,9 +67,10 @@ class NativeHandle:
             _lib.check(lib.pdm_uvit_set_param(h, name.encode(), ctypes.c_void_p(t.data_ptr()), dt.value, t.numel()),
                        "pdm_uvit_set_param")
         _lib.check(lib.pdm_uvit_validate(h), "pdm_uvit_validate")
+        self._mx = {}
 
     @staticmethod
-    def _ln_fold(sd, name):
+    def _ln_fold(sd, name, fp32=False):
         """norm1 -> attn.qkv and norm2 -> mlp.fc1 are fused (libs/uvit.py:115-120): LN(x) W^T + b =
         rstd * (x (W diag(g))^T - mean * colsum) + (W beta + b).  Returns the packed tensor for the folded
         weight / its row sums / the folded bias, or None when `name` is not one of them."""
@@ -77,6 +81,8 @@ class NativeHandle:
                 pre = name[: -len(lin + part)]
                 w = sd[pre + lin + ".weight"].detach().float()
                 g = sd[pre + norm + ".weight"].detach().float()
+                if part == ".weight" and fp32:
+                    return w * g[None, :]
                 wg = (w * g[None, :]).to(torch.bfloat16)
                 if part == ".weight":
                     return wg
@@ -88,8 +94,32 @@ class NativeHandle:
                 return b.float()
         return None
 
-    @staticmethod
-    def _pack(sd, name, dtype, numel, dev):
+    def _mx_weight(self, sd, key, dev):
+        """MXFP8 copy of a block Linear weight [N, K] (norm-folded for attn.qkv / mlp.fc1): e4m3 bytes, E8M0 scale
+        dwords [K/128, N] (the quantiser of the GPU epilogues, _lib.mx_quantize) and the row sums of the
+        DEQUANTISED weight, which the fused LayerNorm subtracts (mean * colsum must cancel exactly what the MFMA
+        multiplies)."""
+        if key not in self._mx:
+            w = self._ln_fold(sd, key, fp32=True)
+            if w is None:
+                w = sd[key].detach().float()
+            q, s = _lib.mx_quantize(w.to(dev))
+            self._mx[key] = (q, s, _lib.mx_dequantize(q, s).double().sum(1).float())
+        return self._mx[key]
+
+    def _pack(self, sd, name, dtype, numel, dev):
+        if self.cfg.fp8:
+            t = None
+            if dtype == _lib.PDM_FP8:
+                t = self._mx_weight(sd, name, dev)[0].view(torch.uint8).reshape(-1)
+            elif dtype == _lib.PDM_E8M0:
+                t = self._mx_weight(sd, name[: -len("_scale")], dev)[1].reshape(-1)
+            elif name.endswith(".ln_colsum"):
+                t = self._mx_weight(sd, name[: -len(".ln_colsum")] + ".weight", dev)[2]
+            if t is not None:
+                if t.numel() != numel:
+                    raise RuntimeError(f"parameter {name!r}: {t.numel()} elements, the HIP layout expects {numel}")
+                return t.contiguous()
         folded = NativeHandle._ln_fold(sd, name)
         if folded is not None:
             t = folded.to(device=dev, dtype=torch.bfloat16 if dtype == _lib.PDM_BF16 else torch.float32)

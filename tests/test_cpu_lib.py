@@ -108,3 +108,44 @@ def test_int2bits_roundtrip(golden):
     back = utils.bits2int(bits > 0)
     np.testing.assert_array_equal(back.numpy(), golden["utils/bits2int"])
     assert utils.amortize(103, 25) == [25, 25, 25, 25, 3]
+
+
+def test_fp8_param_table_without_gpu():
+    """MXFP8 handle (BASELINE configs[4]): every block Linear is an e4m3 [N][K] byte weight with an E8M0
+    [K/128][N] scale companion; the rest of the table is the bf16 one; t2i and non-128 widths are rejected."""
+    import ctypes
+
+    from panopticdiffusionmodels_amd import _lib, configs, native
+    lib = _lib.load()
+    kw = configs.nnet_kwargs("imagenet512_uvit_huge")
+    kw.pop("name")
+    kw["fp8"] = True
+    h = ctypes.c_void_p()
+    _lib.check(lib.pdm_uvit_create(ctypes.byref(native.cfg_struct(kw, False)), ctypes.byref(h)))
+    table = {}
+    buf = ctypes.create_string_buffer(256)
+    for i in range(lib.pdm_uvit_param_count(h)):
+        dt, ne = ctypes.c_int(), ctypes.c_longlong()
+        _lib.check(lib.pdm_uvit_param_info(h, i, buf, 256, ctypes.byref(dt), ctypes.byref(ne)))
+        table[buf.value.decode()] = (dt.value, ne.value)
+    D, Hd = 1152, 4608
+    for key, (N, K) in {"out_blocks.3.attn.qkv.weight": (3 * D, D), "mid_block.attn.proj.weight": (D, D),
+                        "in_blocks.0.mlp.fc1.weight": (Hd, D), "in_blocks.13.mlp.fc2.weight": (D, Hd)}.items():
+        assert table[key] == (_lib.PDM_FP8, N * K), key
+        assert table[key + "_scale"] == (_lib.PDM_E8M0, K // 128 * N), key
+    assert table["decoder_pred.weight"][0] == _lib.PDM_BF16
+    assert table["out_blocks.0.skip_linear.weight"] == (_lib.PDM_BF16, 2 * D * D)
+    ws8, ws16 = ctypes.c_size_t(), ctypes.c_size_t()
+    _lib.check(lib.pdm_uvit_workspace_size(h, 100, ctypes.byref(ws8)))
+    lib.pdm_uvit_destroy(h)
+    kw["fp8"] = False
+    _lib.check(lib.pdm_uvit_create(ctypes.byref(native.cfg_struct(kw, False)), ctypes.byref(h)))
+    _lib.check(lib.pdm_uvit_workspace_size(h, 100, ctypes.byref(ws16)))
+    lib.pdm_uvit_destroy(h)
+    assert 0 < ws8.value < ws16.value   # MXFP8 operands replace the bf16 copies
+    for name, t2i in (("tiny_uvit_h", False), ("tiny_t2i", True)):   # D = 576; t2i
+        k2 = configs.nnet_kwargs(name)
+        k2.pop("name")
+        k2["fp8"] = True
+        with pytest.raises(ValueError):
+            _lib.check(lib.pdm_uvit_create(ctypes.byref(native.cfg_struct(k2, t2i)), ctypes.byref(h)))

@@ -11,11 +11,13 @@ from panopticdiffusionmodels_amd.utils import get_nnet  # noqa: E402
 name = sys.argv[1] if len(sys.argv) > 1 else "imagenet256_uvit_large"
 rows = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 10   # timed forwards
+precision = sys.argv[4] if len(sys.argv) > 4 else "bf16"
 dev = torch.device("cuda")
 cfg = configs.nnet_kwargs(name)
 sd = weights.nnet_state_dict(cfg, seed=0, device=dev)
 net = get_nnet(**cfg).to(dev)
 net.load_state_dict(sd)
+net.set_precision(precision)
 zs = configs.get_config(name)["z_shape"]
 x = torch.randn(rows, *zs, device=dev)
 t = torch.rand(rows, device=dev) * 999
@@ -33,4 +35,4 @@ D, depth = cfg["embed_dim"], cfg["depth"]
 L = (cfg["img_size"] // cfg["patch_size"]) ** 2 + (2 if cfg.get("num_classes", -1) > 0 else 1)
 gemm_flops = rows * L * (depth + 1) * 2 * (3 * D * D + D * D + 8 * D * D) + rows * L * (depth // 2) * 2 * 2 * D * D
 attn_flops = rows * (depth + 1) * 4 * L * L * D
-print(f"{name} rows={rows}: {dt*1e3:.2f} ms/forward, {(gemm_flops+attn_flops)/dt/1e12:.1f} TFLOP/s")
+print(f"{name} {precision} rows={rows}: {dt*1e3:.2f} ms/forward, {(gemm_flops+attn_flops)/dt/1e12:.1f} TFLOP/s")
