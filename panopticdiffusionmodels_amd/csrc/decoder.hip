@@ -23,80 +23,78 @@ namespace pdm {
 namespace {
 
 // ---------------------------------------------------------------------------------------------------
-// GroupNorm statistics: grid (nchunk, B); each block reduces PIX pixels x C channels in fp64 (sum, sumsq)
-// per group, partials -> [B, nchunk, 32, 2]; gn_final combines them into (mean, rstd) per (b, g).
-constexpr int GN_PIX = 64;
+// GroupNorm statistics: grid (nchunk, B); each block reduces `pix` pixels x C channels in fp64 (sum, sumsq)
+// per group, partials -> [B, nchunk, 32, 2]; gn_final combines them into (mean, rstd) per (b, g).  pix is chosen
+// per level so that a block streams ~256 KiB (gn_pix below): 64-pixel chunks left every block latency-bound.
+constexpr int GN_PIX = 64;   // smallest chunk (sizes the partials buffer)
+inline int gn_pix(int C) { return C >= 1024 ? GN_PIX : 65536 / C; }
 
 template <typename T>
-__global__ __launch_bounds__(256) void gn_partial_kernel(const T* x, int P, int C, int nchunk, double* part) {
+__global__ __launch_bounds__(256) void gn_partial_kernel(const T* x, int P, int C, int nchunk, int pix, double* part) {
+  // thread -> one channel quad q of pixel lane `plane` (C <= 1024): per-channel fp32 sums over its <= pix/planes
+  // pixels in registers (compile-time indexed: a runtime group index sent the accumulators to scratch), then
+  // one fp64 pass per group over the [plane][channel] partials in LDS
+  __shared__ float2 red[1024];
   const int b = blockIdx.y, chunk = blockIdx.x;
-  const int cpg = C / 32;
-  __shared__ double s_sum[32], s_sq[32];
-  if (threadIdx.x < 32) { s_sum[threadIdx.x] = 0.0; s_sq[threadIdx.x] = 0.0; }
-  __syncthreads();
-  const int p0 = chunk * GN_PIX;
-  const int p1 = min(P, p0 + GN_PIX);
-  const T* xb = x + (size_t)b * P * C;
-  // thread -> 4 consecutive channels; lanes stride over channels, then pixels
-  const int nq = C / 4;
-  // a quad of channels spans at most two groups (cpg = C/32 >= 2): accumulate lo/hi group separately
-  double su[2][2] = {{0.0, 0.0}, {0.0, 0.0}}, sq[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
-  int glo[2] = {-1, -1}, ghi[2] = {-1, -1}, split[2] = {4, 4};
-  for (int q = threadIdx.x % nq, k = 0; k < 2 && q < nq; q += 256, ++k) {
-    glo[k] = (q * 4) / cpg;
-    ghi[k] = (q * 4 + 3) / cpg;
-    split[k] = (glo[k] + 1) * cpg - q * 4;   // channels j < split belong to glo
-  }
-  const int plane = threadIdx.x / nq;          // pixel lane (C < 1024)
-  const int planes = max(1, 256 / nq);
-  for (int pi = p0 + plane; pi < p1; pi += planes) {
-    const T* row = xb + (size_t)pi * C;
-    int k = 0;
-    for (int q = threadIdx.x % nq; q < nq && k < 2; q += 256, ++k) {
+  const int nq = C >> 2, q = threadIdx.x % nq, plane = threadIdx.x / nq, planes = 256 / nq;
+  const int p0 = chunk * pix, p1 = min(P, p0 + pix);
+  if (plane < planes) {
+    const T* xb = x + (size_t)b * P * C + q * 4;
+    float su[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int pi = p0 + plane; pi < p1; pi += planes) {
       float v[4];
       if constexpr (sizeof(T) == 4) {
-        const f32x4 t = *reinterpret_cast<const f32x4*>(row + q * 4);
+        const f32x4 t = *reinterpret_cast<const f32x4*>(xb + (size_t)pi * C);
         v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
       } else {
-        const bf16x4 t = *reinterpret_cast<const bf16x4*>(row + q * 4);
+        const bf16x4 t = *reinterpret_cast<const bf16x4*>(xb + (size_t)pi * C);
         v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int h = j >= split[k] ? 1 : 0;
-        su[k][h] += v[j];
-        sq[k][h] += v[j] * v[j];
+        su[j] += v[j];
+        sq[j] = fmaf(v[j], v[j], sq[j]);
       }
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[plane * C + q * 4 + j] = make_float2(su[j], sq[j]);
   }
-  for (int k = 0; k < 2; ++k)
-    if (glo[k] >= 0 && threadIdx.x < nq * planes) {
-      atomicAdd(&s_sum[glo[k]], su[k][0]);
-      atomicAdd(&s_sq[glo[k]], sq[k][0]);
-      if (ghi[k] != glo[k]) {
-        atomicAdd(&s_sum[ghi[k]], su[k][1]);
-        atomicAdd(&s_sq[ghi[k]], sq[k][1]);
-      }
-    }
   __syncthreads();
   if (threadIdx.x < 32) {
-    double* o = part + (((size_t)b * nchunk + chunk) * 32 + threadIdx.x) * 2;
-    o[0] = s_sum[threadIdx.x];
-    o[1] = s_sq[threadIdx.x];
+    const int g = threadIdx.x, cpg = C / 32;
+    double s = 0.0, qq = 0.0;
+    for (int pl = 0; pl < planes; ++pl)
+      for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+        const float2 r = red[pl * C + c];
+        s += r.x;
+        qq += r.y;
+      }
+    double* o = part + (((size_t)b * nchunk + chunk) * 32 + g) * 2;
+    o[0] = s;
+    o[1] = qq;
   }
 }
 
+// one wave per (b, g): lanes stride over the chunks, then a wave reduction (a serial per-thread loop over the
+// chunks was a chain of dependent global loads, ~135 us per call)
 __global__ __launch_bounds__(256) void gn_final_kernel(const double* part, int nchunk, double count, float eps,
                                                        float* stats, int B) {
-  const int i = blockIdx.x * 256 + threadIdx.x;   // (b, g)
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;   // (b, g)
   if (i >= B * 32) return;
   const int b = i / 32, g = i % 32;
   double s = 0.0, q = 0.0;
-  for (int c = 0; c < nchunk; ++c) {
+  for (int c = lane; c < nchunk; c += 64) {
     const double* o = part + (((size_t)b * nchunk + c) * 32 + g) * 2;
     s += o[0];
     q += o[1];
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    q += __shfl_xor(q, o, 64);
+  }
+  if (lane) return;
   const double mean = s / count;
   double var = q / count - mean * mean;
   var = var < 0.0 ? 0.0 : var;
@@ -207,15 +205,97 @@ __global__ __launch_bounds__(256) void transpose_kernel(const bf16* src, int ld,
   }
 }
 
-// [B, HW, ldc] fp32 (first C channels) -> [B, C, H, W] fp32
-__global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(const float* in, int ldc, float* out, int HW, int C,
-                                                           int B) {
-  const long long total = (long long)B * C * HW;
-  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-    const int p = (int)(e % HW);
-    const long long bc = e / HW;
-    const int c = (int)(bc % C), b = (int)(bc / C);
-    out[e] = in[((size_t)b * HW + p) * ldc + c];
+// conv_out (libs/autoencoder.py:408-409): 3x3 conv, Cin -> out_ch <= 4, on the GN+swish bf16 NHWC input, written
+// straight to the NCHW fp32 image.  N = 3 is far too narrow for an MFMA tile (a 128-wide tile wastes 97 % of
+// its work), so one thread computes one pixel's outputs on the VALU: 9 taps x Cin/8 16-byte loads (neighbour
+// rows come from L1 / L2); the weights are staged once per block into LDS as fp32 [tap][ci][4 outputs], so each
+// input channel costs one broadcast ds_read_b128 + 4 FMAs (per-lane weight loads from global cost 4x the input
+// bandwidth).
+__global__ __launch_bounds__(256) void conv_out_kernel(const bf16* g, int B, int H, int W, int C, const bf16* w,
+                                                       const float* bias, float* img, int out_ch) {
+  extern __shared__ __attribute__((aligned(16))) f32x4 wl[];   // [9 * C]
+  for (int i = threadIdx.x; i < 9 * C; i += 256)
+    wl[i] = f32x4{(float)w[i], (float)w[9 * C + i], (float)w[18 * C + i], (float)w[27 * C + i]};
+  __syncthreads();
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= (long long)B * H * W) return;
+  const int b = (int)(pix / ((long long)H * W));
+  const int r = (int)(pix - (long long)b * H * W), y = r / W, x = r - (r / W) * W;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int tap = 0; tap < 9; ++tap) {
+    const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+    if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
+    const bf16* src = g + (((size_t)b * H + yy) * W + xx) * C;
+    const f32x4* wt = wl + tap * C;
+    for (int c0 = 0; c0 < C; c0 += 8) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(src + c0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += (float)v[j] * wt[c0 + j];
+    }
+  }
+  for (int o = 0; o < out_ch; ++o) img[((size_t)b * out_ch + o) * H * W + r] = acc[o] + bias[o];
+}
+
+// The same conv for C = 8 * LPP in {64, 128} (every shipped decoder): LPP consecutive lanes share one pixel and
+// each loads 16 contiguous bytes of it, so a wave-instruction reads whole 128-B lines (one pixel per lane read a
+// 16-B piece of 64 different lines per instruction, 4.2 ms for 32 images at 256^2).  A lane keeps its 8
+// channels' weights of one tap in registers across the wave's 16 pixel groups; the LPP partial sums of a pixel
+// are combined with xor-shuffles.
+template <int LPP>
+__global__ __launch_bounds__(256) void conv_out8_kernel(const bf16* g, int B, int H, int W, const bf16* w,
+                                                        const float* bias, float* img, int out_ch) {
+  constexpr int C = LPP * 8, NPG = 64 / LPP, IT = 16;
+  __shared__ f32x4 wl[9 * C];
+  for (int i = threadIdx.x; i < 9 * C; i += 256)
+    wl[i] = f32x4{(float)w[i], (float)w[9 * C + i], (float)w[18 * C + i], (float)w[27 * C + i]};
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane / LPP, ch = (lane % LPP) * 8;
+  const long long npix = (long long)B * H * W;
+  const long long base = ((long long)blockIdx.x * 4 + wave) * (NPG * IT) + sub;
+  int pyx[IT];         // (y << 16) | x of the lane's pixel in group `it`, -1 past the end
+  long long prow[IT];  // first element of that pixel's image
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const long long p = base + it * NPG;
+    if (p < npix) {
+      const int b = (int)(p / ((long long)H * W)), r = (int)(p - (long long)b * H * W);
+      pyx[it] = ((r / W) << 16) | (r % W);
+      prow[it] = (long long)b * H * W;
+    } else {
+      pyx[it] = -1;
+      prow[it] = 0;
+    }
+  }
+  f32x4 acc[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) acc[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int tap = 0; tap < 9; ++tap) {
+    const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+    f32x4 wv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wv[j] = wl[tap * C + ch + j];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int yy = (pyx[it] >> 16) + dy, xx = (pyx[it] & 0xffff) + dx;
+      if (pyx[it] >= 0 && yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(g + (prow[it] + (long long)yy * W + xx) * C + ch);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[it] += (float)v[j] * wv[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+#pragma unroll
+    for (int off = 1; off < LPP; off <<= 1)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) acc[it][o] += __shfl_xor(acc[it][o], off, 64);
+    if (lane % LPP == 0 && pyx[it] >= 0) {
+      const long long p = base + it * NPG;
+      const int b = (int)(p / ((long long)H * W)), r = (int)(p - (long long)b * H * W);
+      for (int o = 0; o < out_ch; ++o) img[((size_t)b * out_ch + o) * H * W + r] = acc[it][o] + bias[o];
+    }
   }
 }
 
@@ -294,7 +374,6 @@ struct DWork {
   bf16* P;        // probabilities [B, hw, hw]
   bf16* VT;       // V^T [B, C, hw]
   bf16* O;        // attention output [B*hw, C]
-  float* OUT4;    // conv_out [B*HW, 4]
   double* part;   // GN partials
   float* stats;   // GN (mean, rstd) [B, 32, 2]
   bf16* zero;     // 256 zero bytes
@@ -336,7 +415,6 @@ DWork dlayout(const pdm_decoder* d, int B, char* base) {
   w.P = (bf16*)take((size_t)B * hw * hw * 2);
   w.VT = (bf16*)take((size_t)B * hw * d->top_ch * 2);
   w.O = (bf16*)take((size_t)B * hw * d->top_ch * 2);
-  w.OUT4 = (float*)take((size_t)B * res * res * 4 * 4);
   w.part = (double*)take((size_t)B * ((size_t)res * res / GN_PIX + 1) * 32 * 2 * sizeof(double));
   w.stats = (float*)take((size_t)B * 32 * 2 * 4);
   w.zero = (bf16*)take(256);
@@ -352,9 +430,10 @@ struct DCtx {
 
 template <typename T>
 int groupnorm(const DCtx& c, const T* x, int B, int P, int C, const std::string& norm, bf16* y, bool swish) {
-  const int nchunk = (P + pdm::GN_PIX - 1) / pdm::GN_PIX;
-  hipLaunchKernelGGL(pdm::gn_partial_kernel<T>, dim3(nchunk, B), dim3(256), 0, c.s, x, P, C, nchunk, c.w->part);
-  hipLaunchKernelGGL(pdm::gn_final_kernel, dim3((B * 32 + 255) / 256), dim3(256), 0, c.s, c.w->part, nchunk,
+  const int pix = pdm::gn_pix(C);
+  const int nchunk = (P + pix - 1) / pix;
+  hipLaunchKernelGGL(pdm::gn_partial_kernel<T>, dim3(nchunk, B), dim3(256), 0, c.s, x, P, C, nchunk, pix, c.w->part);
+  hipLaunchKernelGGL(pdm::gn_final_kernel, dim3((B * 32 + 3) / 4), dim3(256), 0, c.s, c.w->part, nchunk,
                      (double)P * (C / 32), 1e-6f, c.w->stats, B);
   const long long n = (long long)B * P * (C / 4);
   hipLaunchKernelGGL(pdm::gn_apply_kernel<T>, dim3(pdm::gridn(n)), dim3(256), 0, c.s, x, c.w->stats,
@@ -458,6 +537,8 @@ int pdm_decoder_create(const pdm_decoder_cfg* cfg, pdm_decoder** out) {
   for (int i = 0; i < c.num_levels; ++i)
     if ((c.ch * c.ch_mult[i]) % 64) return dfail(PDM_ERR_ARG, "decoder: channel counts must be multiples of 64");
   if (c.latent_size % 8 || c.latent_size > 64) return dfail(PDM_ERR_ARG, "decoder: latent size must be a multiple of 8, <= 64");
+  for (int i = 0; i < c.num_levels; ++i)
+    if (c.ch * c.ch_mult[i] > 1024) return dfail(PDM_ERR_ARG, "decoder: channel counts must be <= 1024");
   pdm_decoder* d = new pdm_decoder();
   d->cfg = c;
   d->nlev = c.num_levels;
@@ -567,9 +648,20 @@ int pdm_decoder_decode(pdm_decoder* d, const float* z, float* img, int B, void* 
     }
   }
   D_TRY(groupnorm<float>(c, X, B, res * res, cin, "decoder.norm_out", w.G, true));
-  D_TRY(conv3(c, w.G, B, res, cin, 4, "decoder.conv_out", pdm::EPI_F32, nullptr, w.OUT4, 0));
-  hipLaunchKernelGGL(pdm::nhwc_to_nchw_kernel, dim3(pdm::gridn((long long)B * d->cfg.out_ch * res * res)), dim3(256), 0,
-                     s, w.OUT4, 4, img, res * res, d->cfg.out_ch, B);
+  {
+    const long long npix = (long long)B * res * res;
+    const bf16* cw = d->w("decoder.conv_out.weight");
+    const float* cb = d->f("decoder.conv_out.bias");
+    if (cin == 128)
+      hipLaunchKernelGGL(pdm::conv_out8_kernel<16>, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, w.G, B, res,
+                         res, cw, cb, img, d->cfg.out_ch);
+    else if (cin == 64)
+      hipLaunchKernelGGL(pdm::conv_out8_kernel<8>, dim3((unsigned)((npix + 511) / 512)), dim3(256), 0, s, w.G, B, res,
+                         res, cw, cb, img, d->cfg.out_ch);
+    else
+      hipLaunchKernelGGL(pdm::conv_out_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 9 * cin * 16, s, w.G,
+                         B, res, res, cin, cw, cb, img, d->cfg.out_ch);
+  }
   D_HIP(hipGetLastError());
   return PDM_OK;
 }
