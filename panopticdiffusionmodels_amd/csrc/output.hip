@@ -5,6 +5,10 @@
 //   utils.py:490-518 bits2int(pred_mask > 0) + utils.py:532-543 color_map: id = sum_i (b_i > 0) 2^(n-1-i),
 //   rgb = colormap[id]
 // Each float op is rounded separately (no contraction), as the reference's separate tensor ops are.
+// Non-finite input: fmaxf/fminf map NaN to 0, so a NaN pixel is written as 0.  torch's clamp_ keeps the NaN and
+// its float -> uint8 cast of NaN is undefined (0 on the x86 host path), so this is the one case where the output
+// is defined here and not in the reference; ±inf saturate exactly as the torch ops do.  A diverged sample is still
+// visible upstream: output.py images_to_u8 counts non-finite values and warns before quantising.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>

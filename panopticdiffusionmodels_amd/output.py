@@ -9,6 +9,7 @@ the wandb/FID plumbing.
                       utils.py:629-635), images under `path`, colour masks under `mask_path`
 """
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -24,10 +25,15 @@ def default_colormap(seed=0):
     return torch.randint(0, 255, (256, 3), generator=g)
 
 
-def images_to_u8(img):
+def images_to_u8(img, check_finite=True):
+    """check_finite: warn when the batch holds NaN/inf (the kernel writes NaN pixels as 0, csrc/output.hip)."""
     lib = _lib.load()
     _lib.require_gpu(img)
     img = img.float().contiguous()
+    if check_finite:
+        bad = int((~torch.isfinite(img)).sum())
+        if bad:
+            warnings.warn(f"images_to_u8: {bad} non-finite values in the decoded batch (written as 0 / 255)")
     B, C, H, W = img.shape
     out = torch.empty(B, H, W, C, dtype=torch.uint8, device=img.device)
     _lib.check(lib.pdm_images_to_u8(_lib.ptr(img), _lib.ptr(out), B, C, H, W, _lib.stream_ptr(img.device)),

@@ -32,15 +32,29 @@ def sample_inputs(indices, z_shape, num_classes=None, seed=1234):
 
 
 def gather_latents(z_local, group=None):
-    """All-gather equally sized per-rank latent batches -> [world * B, ...] in rank order."""
+    """All-gather per-rank latent batches -> [sum of rank sizes, ...] in rank order.
+
+    Ranks may hold different counts (shard() gives sizes that differ by one when n_total % world != 0): the
+    sizes are exchanged first, every shard is padded to the largest, gathered with one equal-size collective,
+    and the padding is trimmed, so the result is the concatenation of the shards in rank order."""
     if not dist.is_available() or not dist.is_initialized():
         return z_local
     world = dist.get_world_size(group)
-    out = torch.empty((world * z_local.shape[0],) + tuple(z_local.shape[1:]), dtype=z_local.dtype,
-                      device=z_local.device)
+    z_local = z_local.contiguous()
+    n = torch.tensor([z_local.shape[0]], dtype=torch.int64, device=z_local.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    bmax = max(sizes)
+    if z_local.shape[0] < bmax:
+        pad = z_local.new_zeros((bmax - z_local.shape[0],) + tuple(z_local.shape[1:]))
+        z_local = torch.cat([z_local, pad])
+    out = torch.empty((world * bmax,) + tuple(z_local.shape[1:]), dtype=z_local.dtype, device=z_local.device)
     if z_local.is_cuda:
-        dist.all_gather_into_tensor(out, z_local.contiguous(), group=group)
+        dist.all_gather_into_tensor(out, z_local, group=group)
     else:  # gloo
         parts = list(out.chunk(world))
-        dist.all_gather(parts, z_local.contiguous(), group=group)
-    return out
+        dist.all_gather(parts, z_local, group=group)
+    if all(s == bmax for s in sizes):
+        return out
+    return torch.cat([out[r * bmax:r * bmax + sizes[r]] for r in range(world)])

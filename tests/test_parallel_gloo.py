@@ -51,8 +51,8 @@ def test_seeding_is_world_size_invariant():
         assert torch.equal(torch.cat([p[1] for p in parts]), y_all)
 
 
-def test_gather_world2_gloo():
-    n = 8
+@pytest.mark.parametrize("n", [8, 7])   # 7: ragged shards (4 + 3)
+def test_gather_world2_gloo(n):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
