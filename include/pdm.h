@@ -43,7 +43,8 @@ int pdm_device_arch(char* buf, int len);
  *   GEMM: 1 = 128x128, 2 = 256x256 BK32 ring, 3 = 256x256 BK64 ring, 4 = 256x256 8-phase staggered
  *   attention: 1 = streamed K/V per 64-query block, 2 / 3 = head-resident K/V with 2 / 3 query tiles per wave */
 /* GEMM tile-order knob: raster = row panels per tile group inside an XCD's tile range (0 = row-major);
- * dbg_tile0 != 0 stages every tile's operands from tile (0, 0) -- a timing experiment, results are wrong */
+ * dbg_tile0 bit 0 stages every tile's operands from tile (0, 0); bit 1 lets a bf16 GEMM run with no output (mainloop +
+ * LDS staging only) -- timing experiments, results are wrong */
 int pdm_set_gemm_tuning(int raster, int dbg_tile0);
 int pdm_set_gemm_algo(int algo);
 int pdm_set_attention_algo(int algo);
