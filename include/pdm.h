@@ -236,6 +236,35 @@ int pdm_images_to_u8(const float* img, uint8_t* out, int B, int C, int H, int W,
 int pdm_mask_bits_to_rgb(const float* bits, int nbits, const int32_t* colormap, int32_t* ids, uint8_t* rgb, int B,
                          int H, int W, void* stream);
 
+/* ---- CLIP text encoder: the t2i conditioning producer (libs/clip.py:13-38 FrozenCLIPEmbedder.encode =
+ * transformers CLIPTextModel(input_ids).last_hidden_state, openai/clip-vit-large-patch14) -------------
+ * Input: token ids int64 [B, L] (L <= max_position; the reference pads to 77 with padding="max_length");
+ * output: fp32 [B, L, width].  Weights under the CLIPTextModel state_dict keys (without "text_model."), with:
+ *   encoder.layers.i.self_attn.{q,k,v}_proj packed into ".self_attn.qkv.weight" bf16 [3W][W] and
+ *   layer_norm1 / layer_norm2 folded into qkv / mlp.fc1 like the U-ViT blocks: ".weight" = bf16(W diag(gamma)),
+ *   ".ln_colsum" f32 = row sums of that bf16 weight, ".ln_bias" f32 = W beta + b;
+ *   out_proj / fc2: bf16 [N][K] + f32 bias; embeddings and final_layer_norm: fp32 in the reference layout. */
+typedef struct pdm_clip pdm_clip;
+
+typedef struct pdm_clip_cfg {
+  int vocab;         /* 49408 */
+  int width;         /* 768 */
+  int layers;        /* 12 */
+  int heads;         /* 12 (head dim 64; 32 also supported) */
+  int mlp_hidden;    /* 3072 */
+  int max_position;  /* 77 (<= 128) */
+  float eps;         /* 1e-5 */
+} pdm_clip_cfg;
+
+int pdm_clip_create(const pdm_clip_cfg* cfg, pdm_clip** out);
+int pdm_clip_destroy(pdm_clip* c);
+int pdm_clip_param_count(const pdm_clip* c);
+int pdm_clip_param_info(const pdm_clip* c, int i, char* name, int len, int* dtype, long long* numel);
+int pdm_clip_set_param(pdm_clip* c, const char* name, const void* dev_ptr, int dtype, long long numel);
+int pdm_clip_workspace_size(const pdm_clip* c, int batch, size_t* bytes);
+int pdm_clip_encode(pdm_clip* c, const int64_t* ids, int batch, int L, float* out, void* workspace,
+                    size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -29,6 +29,11 @@ class PdmDecoderCfg(ctypes.Structure):
                 ("latent_size", ctypes.c_int), ("scale_factor", ctypes.c_float)]
 
 
+class PdmClipCfg(ctypes.Structure):
+    _fields_ = [("vocab", ctypes.c_int), ("width", ctypes.c_int), ("layers", ctypes.c_int), ("heads", ctypes.c_int),
+                ("mlp_hidden", ctypes.c_int), ("max_position", ctypes.c_int), ("eps", ctypes.c_float)]
+
+
 class PdmStageEpilogueArgs(ctypes.Structure):
     _fields_ = [
         ("pre", ctypes.c_void_p), ("conv_w", ctypes.c_void_p), ("conv_b", ctypes.c_void_p),
@@ -115,6 +120,16 @@ _SIGS = {
                                         ctypes.c_int, ctypes.c_void_p]),
     "pdm_mask_bits_to_rgb": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    "pdm_clip_create": (ctypes.c_int, [ctypes.POINTER(PdmClipCfg), ctypes.POINTER(ctypes.c_void_p)]),
+    "pdm_clip_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "pdm_clip_param_count": (ctypes.c_int, [ctypes.c_void_p]),
+    "pdm_clip_param_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_longlong)]),
+    "pdm_clip_set_param": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int,
+                                          ctypes.c_longlong]),
+    "pdm_clip_workspace_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
+    "pdm_clip_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "pdm_decoder_create": (ctypes.c_int, [ctypes.POINTER(PdmDecoderCfg), ctypes.POINTER(ctypes.c_void_p)]),
     "pdm_decoder_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "pdm_decoder_param_count": (ctypes.c_int, [ctypes.c_void_p]),

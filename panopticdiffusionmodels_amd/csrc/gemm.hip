@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p, int tiles
         *reinterpret_cast<bf16x4*>(p.out_bf16 + (size_t)m * p.ldo + n) = to_bf16x4(v[0], v[1], v[2], v[3]);
       } else if constexpr (EPI == EPI_GELU) {
         *reinterpret_cast<bf16x4*>(p.out_bf16 + (size_t)m * p.ldo + n) =
-            to_bf16x4(gelu_erf(v[0]), gelu_erf(v[1]), gelu_erf(v[2]), gelu_erf(v[3]));
+            to_bf16x4(gelu_act(p.act, v[0]), gelu_act(p.act, v[1]), gelu_act(p.act, v[2]), gelu_act(p.act, v[3]));
       } else {
         f32x4* r = reinterpret_cast<f32x4*>(p.out_f32 + (size_t)m * p.ldr + n);
         if (p.accumulate) v += *r;
@@ -268,7 +268,11 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
         }
         v += bv[gi];
         if constexpr (EPI == EPI_GELU) {
-          v[0] = gelu_erf(v[0]); v[1] = gelu_erf(v[1]); v[2] = gelu_erf(v[2]); v[3] = gelu_erf(v[3]);
+          if (p.act) {
+            v[0] = gelu_quick(v[0]); v[1] = gelu_quick(v[1]); v[2] = gelu_quick(v[2]); v[3] = gelu_quick(v[3]);
+          } else {
+            v[0] = gelu_erf(v[0]); v[1] = gelu_erf(v[1]); v[2] = gelu_erf(v[2]); v[3] = gelu_erf(v[3]);
+          }
         }
         const int off = ml * 512 + ((((nl >> 3) ^ (ml & 31)) << 4) | ((nl & 4) << 1));
         *reinterpret_cast<bf16x4*>(smem + off) = to_bf16x4(v[0], v[1], v[2], v[3]);

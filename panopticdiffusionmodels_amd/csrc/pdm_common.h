@@ -44,6 +44,10 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return fmaf(-0.5f * a, r, fmaxf(x, 0.0f));
 }
 
+// quick GELU (transformers QuickGELUActivation, CLIP text encoder): x * sigmoid(1.702 x)
+__device__ __forceinline__ float gelu_quick(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+__device__ __forceinline__ float gelu_act(int act, float x) { return act ? gelu_quick(x) : gelu_erf(x); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -54,6 +54,9 @@ struct GemmArgs {
   // tuning knobs (set by gemm_launch): raster = row panels per tile group inside an XCD's range (0: row-major);
   // dbg_tile0 = stage every tile's operands from tile (0, 0) (timing experiments only: wrong results)
   int raster, dbg_tile0;
+  // EPI_GELU activation: 0 = exact-erf GELU (nn.GELU, libs/timm.py:102), 1 = quick GELU x * sigmoid(1.702 x)
+  // (the CLIP text encoder's hidden_act, transformers CLIPMLP)
+  int act;
 };
 void gemm_set_tuning(int raster, int dbg_tile0);
 
