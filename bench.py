@@ -103,16 +103,11 @@ def main():
 
     ev = []   # (start, after sampling, after decode) HIP events per timed step, on the launch stream
 
-    def one_step(s, profile=False, timed=False):
+    def one_step(s, timed=False):
         if timed:
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record()
-        if profile:   # last timed step: eager launches with HIP events around every GEMM (libpdm hook)
-            prof.enable()
-            z = sampler.sample(zs[s], ys[s], eager=True)
-            prof.disable()
-        else:
-            z = sampler.sample(zs[s], ys[s])
+        z = sampler.sample(zs[s], ys[s])
         if world > 1:
             z = parallel.gather_latents(z)[rank * B:(rank + 1) * B]
         if timed:
@@ -131,7 +126,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.warmup, nsteps):
-        out = one_step(s, profile=(s == nsteps - 1), timed=True)
+        out = one_step(s, timed=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -143,8 +138,13 @@ def main():
         elapsed = float(t.item())
     assert torch.isfinite(out).all()
 
-    # ---- roofline of the dominant kernel (the bf16 GEMM family): HIP events recorded by libpdm on the launch
-    # stream around every GEMM launch of the last forward of the last timed step
+    # ---- roofline of the dominant kernel (the bf16 GEMM family), after the timed region: the last step's inputs
+    # sampled once more eagerly with libpdm's HIP events around every GEMM launch (recorded on the launch stream);
+    # the last forward's launches are read back -- the kernels and shapes of the timed steps
+    prof.enable()
+    sampler.sample(zs[-1], ys[-1], eager=True)
+    prof.disable()
+    torch.cuda.synchronize(dev)
     roof = gemm_roofline(prof, ncfg, 2 * B if sampler.cfg else B, precision)
     samp_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
@@ -171,8 +171,7 @@ def main():
                    "nfe": sampler.nfe, "hip_graph": not args.no_graph, "parallelism": f"dp{world} (batch-sharded)"},
         "roofline": roof,
         "breakdown_ms_per_step": {"sample_50nfe": round(samp_ms, 2), "decode": round(dec_ms, 2),
-                                  "note": "HIP events on the launch stream; the last timed step samples eagerly "
-                                          "with per-GEMM events (graph replay in the others)"},
+                                  "note": "HIP events on the launch stream around each timed step (graph replay)"},
     }
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         res["cpu_baseline"] = cpu_baseline(full, ncfg, ae is not None)
@@ -213,7 +212,8 @@ def gemm_roofline(prof, ncfg, rows, precision="bf16"):
             "achieved": round(achieved / 1e12, 1), "peak": round(peak / 1e12, 1), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic,
             "traffic_source": tsrc,
-            "measured": "HIP events on the launch stream around each GEMM of the last CFG forward of the last timed step",
+            "measured": "HIP events on the launch stream around each GEMM of the last CFG forward of one eager "
+                        "sample of the last step's batch, after the timed region",
             "launches_per_forward": n, "avg_launch_ms": round(tot_t / n * 1e3, 4),
             "flops_per_launch": round(tot_f / n), "flops_per_forward": gemm_flops_per_forward(ncfg, rows)}
 

@@ -127,8 +127,10 @@ class UViT(HipNet):
         return {'pos_embed'}
 
     # ---- HIP path ------------------------------------------------------------------------------
-    def forward_pre(self, x, timesteps, y=None, out=None):
-        """Everything up to the final conv: returns the unpatchified decoder_pred output [B, C, H, W] fp32."""
+    def forward_pre(self, x, timesteps, y=None, out=None, workspace=None):
+        """Everything up to the final conv: returns the unpatchified decoder_pred output [B, C, H, W] fp32.
+        workspace: a caller-owned uint8 device tensor of >= workspace_bytes(B) (default: the handle's own), so
+        independent batches can run concurrently on different streams."""
         _lib.require_gpu(x)
         nat = self.native()
         x = x.float().contiguous()
@@ -145,7 +147,7 @@ class UViT(HipNet):
             y = y.to(device=x.device, dtype=torch.int64).reshape(-1).contiguous()
         if out is None:
             out = torch.empty(B, self.in_chans, self.img_size, self.img_size, dtype=torch.float32, device=x.device)
-        ws = nat.workspace(B, x.device)
+        ws = nat.workspace(B, x.device) if workspace is None else workspace
         _lib.check(nat.lib.pdm_uvit_forward(nat.h, _lib.ptr(x), _lib.ptr(t), _lib.ptr(y), _lib.ptr(out), B,
                                             _lib.ptr(ws), ws.numel(), _lib.stream_ptr(x.device)), "pdm_uvit_forward")
         return out

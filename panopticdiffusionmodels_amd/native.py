@@ -144,6 +144,11 @@ class NativeHandle:
             raise RuntimeError(f"parameter {name!r}: {t.numel()} elements, the HIP layout expects {numel}")
         return t
 
+    def workspace_bytes(self, rows):
+        need = ctypes.c_size_t()
+        _lib.check(self.lib.pdm_uvit_workspace_size(self.h, rows, ctypes.byref(need)), "pdm_uvit_workspace_size")
+        return need.value
+
     def workspace(self, rows, device):
         need = ctypes.c_size_t()
         _lib.check(self.lib.pdm_uvit_workspace_size(self.h, rows, ctypes.byref(need)), "pdm_uvit_workspace_size")
