@@ -41,7 +41,9 @@ int pdm_version(void);
 int pdm_device_arch(char* buf, int len);
 /* Tile-policy overrides for A/B measurement (0 = automatic; the default everywhere).
  *   GEMM: 1 = 128x128, 2 = 256x256 BK32 ring, 3 = 256x256 BK64 ring, 4 = 256x256 8-phase staggered
- *   attention: 1 = streamed K/V per 64-query block, 2 / 3 = head-resident K/V with 2 / 3 query tiles per wave */
+ *   attention: 1 = streamed K/V per 64-query block, 2 / 3 = head-resident K/V with 2 / 3 query tiles per wave,
+ *              4 = head-resident v2 (Dh 64), 7 = head-resident Dh 72 (64 + 8 split); 5/6, 8/9 = their load-only /
+ *              math-only timing variants (wrong results) */
 /* GEMM tile-order knob: raster = row panels per tile group inside an XCD's tile range (0 = row-major);
  * dbg_tile0 bit 0 stages every tile's operands from tile (0, 0); bit 1 lets a bf16 GEMM run with no output (mainloop +
  * LDS staging only) -- timing experiments, results are wrong */

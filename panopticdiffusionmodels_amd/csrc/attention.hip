@@ -614,6 +614,244 @@ __global__ __launch_bounds__(256, 2) void attention_v2_kernel(AttentionArgs p, i
     else run_pass(std::integral_constant<int, 1>{}, qf, tl, pass == 0);
   }
 }
+
+// ------------------------------------------------------------------------------------------------
+// Head-resident kernel for Dh = 72 (U-ViT-H/2 and H/4: libs/uvit.py:66-92 with embed_dim 1152, 16 heads), the
+// v2 structure above with the head dim cut as 64 + 8 instead of padded to 96:
+//   Q K^T: two v_mfma_f32_16x16x32_bf16 k-steps over d 0..63 + one v_mfma_f32_16x16x16_bf16 over d 64..71
+//          (lanes of k-group 2, 3 hold zeros), i.e. 40 instead of 48 MFMA cycles per 16x16 score tile;
+//   P V:   five 16-column output tiles (d 64..79 for the last; rows 72..79 of it are never stored).
+// K and V rows stay unpadded (144 B) so a head's K + V fit twice per CU at L = 258:
+//   LDS = [V rows 0 .. round8(L)) [K rows 0 .. round16(L)), 144 B each; staged by LDS-DMA as a flat array of
+//   16-B chunks (chunk ci -> row ci / 9, column chunk ci % 9).  PV reads whole 32-key steps, so V rows past
+//   round8(L) read the (finite) K rows behind them and are multiplied by P = 0; K rows past round8(L) are never
+//   staged and their scores are masked.  The 144-B stride leaves 2-way bank conflicts on the fragment reads
+//   (no 16-B chunk permutation of a 9-chunk row removes them; the MFMAs, not LDS, bound the loop).
+template <int DEBUG>
+__global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, int nqt, int LV, int L16) {
+  constexpr int DH = 72, ROWB = 144, NCH = 9;
+  constexpr float RESCALE_THR = 8.0f;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* Vs = lds;
+  char* Ks = lds + LV * ROWB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bh = blockIdx.x;
+  const int b = bh / p.H, h = bh % p.H;
+  const int L = p.L, D = p.H * DH;
+  const bf16* base = p.qkv + (size_t)b * L * p.ldq + h * DH;
+  const int g = lane >> 4, col = lane & 15;
+  const bool glo = g < 2;   // k-groups holding d 64..71 in the 16x16x16 remainder step
+
+  const int my_tiles = nqt > wave ? (nqt - wave + 3) / 4 : 0;
+  const int npass = (my_tiles + 1) / 2;
+
+  auto qrow = [&](int tile) {
+    int q = tile * 16 + col;
+    q = q < L ? q : L - 1;
+    return base + (size_t)q * p.ldq;
+  };
+  // Q fragments of the first pass: d = ks*32 + g*8 .. +7 (x32 steps) and d = 64 + 4g .. +3 (x16 step, g < 2)
+  i32x4 q0[2][2];
+  int2 q0r[2];
+  if (npass > 0 && DEBUG != 2) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const bf16* qr = qrow(min(wave + 4 * t, nqt - 1));
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) q0[t][ks] = gload16_asm(qr + ks * 32 + g * 8);
+      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(q0r[t]) : "v"(qr + 64 + 4 * (g & 1)) : "memory");
+    }
+  }
+  // K / V DMA: 64 chunks (1 KiB) per instruction, instruction i of each tensor issued by wave i % 4, V before K
+  const int ndma = (LV * NCH + 63) / 64;
+  if (DEBUG != 2) {
+    for (int i = wave; i < ndma; i += 4) {
+      const int ci = i * 64 + lane;
+      if (ci < LV * NCH) {
+        const int row = ci / NCH, ch = ci - row * NCH;
+        const bf16* src = base + (size_t)(row < L ? row : L - 1) * p.ldq + ch * 8;
+        glds16(src + 2 * D, (PDM_LDS void*)(Vs + i * 1024));
+        glds16(src + D, (PDM_LDS void*)(Ks + i * 1024));
+      }
+    }
+  }
+  // DMA instructions (both tensors) this wave issued past block c: rows < 64 (c + 1) are chunks < 576 (c + 1)
+  auto ops_after = [&](int c) {
+    const int need = min(ndma, 9 * (c + 1));
+    int n = 0;
+    for (int i = wave; i < ndma; i += 4) n += i >= need ? 2 : 0;
+    return n;
+  };
+  auto block_ready = [&](int c) {
+    if (DEBUG == 0) wait_vmcnt_dyn(ops_after(c));
+    else if (DEBUG == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const float sl2 = p.scale * 1.4426950408889634f;
+  const int nfull = L / 64, nch = (L + 63) / 64;
+  const s16x4 zero4 = s16x4{0, 0, 0, 0};
+
+  auto run_pass = [&](auto ntc, const bf16x8 (&qf)[2][2], const s16x4 (&qr)[2], const int (&tl)[2], bool first) {
+    constexpr int NT = decltype(ntc)::value;
+    float m_run[NT], l_run[NT];
+    f32x4 acc[NT][5];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      m_run[t] = -INFINITY;
+      l_run[t] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto do_block = [&](int c, auto tailc) {
+      constexpr bool TAIL = decltype(tailc)::value;
+      const int kvalid = L - c * 64;
+      f32x4 s[NT][4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (TAIL && kt * 16 >= kvalid) continue;
+        const char* krow = Ks + (c * 64 + kt * 16 + col) * ROWB;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + (ks * 4 + g) * 16);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kf, qf[t][ks], s[t][kt]);
+        }
+        s16x4 kr = *reinterpret_cast<const s16x4*>(krow + 128 + 8 * (g & 1));
+        kr = glo ? kr : zero4;
+        // the d 64..71 step accumulates separately and is added by the VALU: a 16x16x16 MFMA reading as SrcC the
+        // result of the 16x16x32 MFMA just before it got too few wait states from hipcc (ROCm 7.2) on gfx950 when
+        // nothing else was interleaved (NT = 1): wrong scores, measured
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          s[t][kt] += __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kr, qr[t], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+      if constexpr (TAIL) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (kt * 16 + g * 4 + j >= kvalid)
+#pragma unroll
+              for (int t = 0; t < NT; ++t) s[t][kt][j] = -INFINITY;
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4 m4 = s[t][0];
+#pragma unroll
+        for (int kt = 1; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) m4[j] = fmaxf(m4[j], s[t][kt][j]);
+        const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]))) * sl2;
+        const bool grow = cmax > m_run[t] + RESCALE_THR;
+        const float m_new = grow ? cmax : m_run[t];
+        const float alpha = __builtin_amdgcn_exp2f(m_run[t] - m_new);
+        m_run[t] = m_new;
+        f32x4 l4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(fmaf(s[t][kt][j], sl2, -m_new));
+          l4 += s[t][kt];
+        }
+        l_run[t] = fmaf(l_run[t], alpha, (l4[0] + l4[1]) + (l4[2] + l4[3]));
+        if (__builtin_amdgcn_ballot_w64(grow)) {
+#pragma unroll
+          for (int i = 0; i < 5; ++i) acc[t][i] *= alpha;
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (TAIL && kk * 32 >= kvalid) break;
+        bf16x8 pf[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pf[t][j] = (bf16)s[t][2 * kk][j];
+            pf[t][4 + j] = (bf16)s[t][2 * kk + 1][j];
+          }
+        const int qq = col >> 2, pp = col & 3;
+        const char* v1 = Vs + (c * 64 + kk * 32 + 4 * g + qq) * ROWB + 8 * pp;
+        const char* v2 = v1 + 16 * ROWB;
+#pragma unroll
+        for (int dt = 0; dt < 5; ++dt) {
+          const s16x4 lo = lds_read_tr16(v1 + dt * 32);
+          const s16x4 hi = lds_read_tr16(v2 + dt * 32);
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf, pf[t], acc[t][dt]);
+        }
+      }
+    };
+    for (int c = 0; c < nfull; ++c) {
+      if (first) block_ready(c);
+      if (DEBUG != 1) do_block(c, std::false_type{});
+    }
+    if (nfull < nch) {
+      if (first) block_ready(nfull);
+      if (DEBUG != 1) do_block(nfull, std::true_type{});
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float inv = 1.0f / xrow_sum(l_run[t]);
+      const int q = tl[t] * 16 + col;
+      if (q < L) {
+        bf16* orow = p.out + ((size_t)b * L + q) * p.ldo + h * DH;
+#pragma unroll
+        for (int dt = 0; dt < 5; ++dt) {
+          if (dt == 4 && !glo) break;   // d 72..79 of the last tile are padding
+          const f32x4 v = acc[t][dt] * inv;
+          *reinterpret_cast<bf16x4*>(orow + dt * 16 + g * 4) = to_bf16x4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+  };
+
+  if (npass == 0) {
+    for (int c = 0; c < nch; ++c) block_ready(c);
+    return;
+  }
+  bf16x8 qf[2][2];
+  s16x4 qr[2];
+  if (DEBUG != 2) {
+    asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]), "+v"(q0r[0]), "+v"(q0r[1]));
+  }
+  for (int pass = 0; pass < npass; ++pass) {
+    const int tl[2] = {wave + 8 * pass, wave + 8 * pass + 4};
+    const bool two = tl[1] < nqt;
+    if (pass == 0) {
+      if (DEBUG == 0) {
+        wait_vmcnt_dyn(ops_after(0));
+        asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]), "+v"(q0r[0]), "+v"(q0r[1]));
+      } else if (DEBUG == 1) {
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]), "+v"(q0r[0]),
+                     "+v"(q0r[1]));
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) qf[t][ks] = __builtin_bit_cast(bf16x8, q0[t][ks]);
+        qr[t] = glo ? __builtin_bit_cast(s16x4, q0r[t]) : zero4;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const bf16* r = qrow(t == 0 || two ? tl[t] : tl[0]);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) qf[t][ks] = *reinterpret_cast<const bf16x8*>(r + ks * 32 + g * 8);
+        const s16x4 v = *reinterpret_cast<const s16x4*>(r + 64 + 4 * (g & 1));
+        qr[t] = glo ? v : zero4;
+      }
+    }
+    if (two) run_pass(std::integral_constant<int, 2>{}, qf, qr, tl, pass == 0);
+    else run_pass(std::integral_constant<int, 1>{}, qf, qr, tl, pass == 0);
+  }
+}
 }  // namespace
 
 const char* attention_check(const AttentionArgs& p) {
@@ -633,6 +871,24 @@ hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream) {
   const int nqt = (p.L + 15) / 16;
   int algo = g_attention_algo;
   const int Lp = (p.L + 31) / 32 * 32;   // PV reads whole 32-key steps
+  // Dh = 72 (U-ViT-H): head-resident 64 + 8 kernel when two heads' K + V fit per CU (L <= 280); 7/8/9 = timing
+  // variants (normal / loads only / math only); measured tools/attn_bench.py
+  const int LV = (p.L + 7) / 8 * 8, L16 = (p.L + 15) / 16 * 16;
+  const int smem72 = (LV + L16) * 144;   // V rows read past LV (up to round32(L)) alias staged K rows below LV
+  if (p.Dh == 72 && smem72 <= 80 * 1024 && (p.L + 31) / 32 * 32 <= 2 * LV && (algo == 0 || (algo >= 7 && algo <= 9))) {
+    static bool attr72 = false;
+    if (!attr72) {
+      (void)hipFuncSetAttribute((const void*)attention_h72_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_h72_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_h72_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      attr72 = true;
+    }
+    const dim3 grid(p.B * p.H), block(256);
+    if (algo == 8) hipLaunchKernelGGL(attention_h72_kernel<1>, grid, block, smem72, stream, p, nqt, LV, L16);
+    else if (algo == 9) hipLaunchKernelGGL(attention_h72_kernel<2>, grid, block, smem72, stream, p, nqt, LV, L16);
+    else hipLaunchKernelGGL(attention_h72_kernel<0>, grid, block, smem72, stream, p, nqt, LV, L16);
+    return hipGetLastError();
+  }
   if (p.Dh != 64 || Lp * 256 > 160 * 1024) algo = 1;
   // automatic: the head-resident v2 structure wherever the head's K/V fit in LDS (Dh = 64: every U-ViT-S/M/L
   // shape); measured 152 vs 213 us (streamed) on L/2 at 190 rows (tools/attn_bench.py)

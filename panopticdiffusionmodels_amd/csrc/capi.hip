@@ -513,7 +513,8 @@ int pdm_set_gemm_tuning(int raster, int dbg_tile0) {
 }
 
 int pdm_set_attention_algo(int algo) {
-  if (algo < 0 || algo > 6) return fail(PDM_ERR_ARG, "pdm_set_attention_algo: algo must be 0 (auto) or 1..6 (5, 6: timing experiments)");
+  if (algo < 0 || algo > 9)
+    return fail(PDM_ERR_ARG, "pdm_set_attention_algo: algo must be 0 (auto) or 1..9 (5, 6, 8, 9: timing experiments)");
   pdm::attention_set_algo(algo);
   return PDM_OK;
 }

@@ -261,6 +261,28 @@ def test_attention_algos(lib, algo, L):
     assert rel(out.float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("L", [33, 66, 129, 257, 258, 280])
+def test_attention_h72(lib, L):
+    """Head-resident Dh = 72 kernel (64 + 8 head-dim split, unpadded 144-B K/V rows; U-ViT-H/2, H/4) at the H
+    head count on ragged lengths, with a dominant key row forcing the deferred-rescale branch."""
+    H, B, Dh = 16, 3, 72
+    D = H * Dh
+    g = torch.Generator(device="cuda").manual_seed(L + 72)
+    qkv = torch.randn(B * L, 3 * D, device="cuda", generator=g) * 1.5
+    qkv[L - 1, D:2 * D] *= 6.0   # the last key of sequence 0 dominates (ragged block)
+    qkv = qkv.bfloat16()
+    lib.check(lib.load().pdm_set_attention_algo(7), "pdm_set_attention_algo")
+    try:
+        out = lib.attention(qkv, B, L, H, Dh)
+    finally:
+        lib.load().pdm_set_attention_algo(0)
+    q, k, v = qkv.float().reshape(B, L, 3, H, Dh).permute(2, 0, 3, 1, 4)
+    ref = torch.softmax(q @ k.transpose(-1, -2) * Dh ** -0.5, dim=-1) @ v
+    ref = ref.permute(0, 2, 1, 3).reshape(B * L, D)
+    assert torch.isfinite(out.float()).all()
+    assert rel(out.float(), ref) < 1e-2
+
+
 def test_attention_spiky(lib):
     """A key row far above the rest forces a late running-max jump (online-softmax rescale branch)."""
     B, L, H, Dh = 1, 258, 2, 64
