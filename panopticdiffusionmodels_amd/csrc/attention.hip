@@ -482,6 +482,16 @@ __global__ __launch_bounds__(256, 2) void attention_v2_kernel(AttentionArgs p, i
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    // LDS addresses: both swizzles are independent of the block c and of kt / kk (row = c*64 + kt*16 + col gives
+    // (row >> 1) & 7 = (col >> 1) & 7; V row r = c*64 + kk*32 + 4g + qq gives (r >> 1) & 3 = (2g + (qq >> 1)) & 3),
+    // so every fragment read is a per-lane base + c * 8 KiB + an immediate offset (no address VALU per read)
+    const char* kbase[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) kbase[ks] = Ks + col * 128 + (((ks * 4 + g) ^ ((col >> 1) & 7)) << 4);
+    const char* vbase[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+      vbase[dt] = Vs + (4 * g + (col >> 2)) * 128 + ((dt ^ ((2 * g + (col >> 3)) & 3)) << 5) + 8 * (col & 3);
     auto do_block = [&](int c, auto tailc) {
       constexpr bool TAIL = decltype(tailc)::value;
       const int kvalid = L - c * 64;
@@ -491,10 +501,9 @@ __global__ __launch_bounds__(256, 2) void attention_v2_kernel(AttentionArgs p, i
 #pragma unroll
         for (int t = 0; t < NT; ++t) s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (TAIL && kt * 16 >= kvalid) continue;
-        const int row = c * 64 + kt * 16 + col;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + row * 128 + (((ks * 4 + g) ^ ((row >> 1) & 7)) << 4));
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbase[ks] + c * 8192 + kt * 2048);
 #pragma unroll
           for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kf, qf[t][ks], s[t][kt]);
         }
@@ -545,12 +554,11 @@ __global__ __launch_bounds__(256, 2) void attention_v2_kernel(AttentionArgs p, i
             pf[t][j] = (bf16)s[t][2 * kk][j];
             pf[t][4 + j] = (bf16)s[t][2 * kk + 1][j];
           }
-        const int qq = col >> 2, pp = col & 3;
-        const int r1 = c * 64 + kk * 32 + 4 * g + qq, r2 = r1 + 16;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
-          const s16x4 lo = lds_read_tr16(Vs + r1 * 128 + ((dt ^ ((r1 >> 1) & 3)) << 5) + 8 * pp);
-          const s16x4 hi = lds_read_tr16(Vs + r2 * 128 + ((dt ^ ((r2 >> 1) & 3)) << 5) + 8 * pp);
+          const char* v1 = vbase[dt] + c * 8192 + kk * 4096;
+          const s16x4 lo = lds_read_tr16(v1);
+          const s16x4 hi = lds_read_tr16(v1 + 2048);
           const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
           for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf, pf[t], acc[t][dt]);
@@ -705,6 +713,8 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
 #pragma unroll
       for (int i = 0; i < 5; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    const char* kbase = Ks + col * ROWB;   // per-lane bases; block / kt / kk / dt offsets are immediates
+    const char* vbase = Vs + (4 * g + (col >> 2)) * ROWB + 8 * (col & 3);
     auto do_block = [&](int c, auto tailc) {
       constexpr bool TAIL = decltype(tailc)::value;
       const int kvalid = L - c * 64;
@@ -714,7 +724,7 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
 #pragma unroll
         for (int t = 0; t < NT; ++t) s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (TAIL && kt * 16 >= kvalid) continue;
-        const char* krow = Ks + (c * 64 + kt * 16 + col) * ROWB;
+        const char* krow = kbase + c * (64 * ROWB) + kt * (16 * ROWB);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + (ks * 4 + g) * 16);
@@ -775,8 +785,7 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
             pf[t][j] = (bf16)s[t][2 * kk][j];
             pf[t][4 + j] = (bf16)s[t][2 * kk + 1][j];
           }
-        const int qq = col >> 2, pp = col & 3;
-        const char* v1 = Vs + (c * 64 + kk * 32 + 4 * g + qq) * ROWB + 8 * pp;
+        const char* v1 = vbase + c * (64 * ROWB) + kk * (32 * ROWB);
         const char* v2 = v1 + 16 * ROWB;
 #pragma unroll
         for (int dt = 0; dt < 5; ++dt) {
