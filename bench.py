@@ -34,7 +34,12 @@ from panopticdiffusionmodels_amd.utils import get_nnet  # noqa: E402
 PEAK_BF16 = 2.5e15   # dense bf16 MFMA, MI355X_MICROARCH.md chip table
 PEAK_FP8 = 5.0e15    # dense MX-fp8 (block-scaled 16x16x128 f8f6f4) MFMA, same table
 MODEL_NAMES = {"imagenet256_uvit_large": "U-ViT-L/2", "imagenet256_uvit_huge": "U-ViT-H/2",
-               "imagenet512_uvit_huge": "U-ViT-H/4", "cifar10_uvit_small": "U-ViT-S/2 (pixel)"}
+               "imagenet512_uvit_huge": "U-ViT-H/4", "cifar10_uvit_small": "U-ViT-S/2 (pixel)",
+               "mscoco_uvit_small": "U-ViT-S/2 t2i + panoptic mask (CLIP ViT-L/14 text encoder)"}
+# algorithmic TFLOP per image (50 NFE x CFG forward + decode; t2i adds the CLIP encoder, 13.1 GF)
+TF_PER_IMAGE = {"imagenet256_uvit_large": 15.913, "imagenet256_uvit_huge": 27.261, "imagenet512_uvit_huge": 29.160,
+                "mscoco_uvit_small": 10.221 + 0.0131, "cifar10_uvit_small": 1.220}
+CLIP_BOS, CLIP_EOS = 49406, 49407
 
 
 def parse():
@@ -82,10 +87,33 @@ def main():
     net.load_state_dict(sd)
     del sd
     precision = full.get("precision", "bf16")   # configs[4]: MXFP8 block Linears (UViT.set_precision)
-    net.set_precision(precision)
+    if hasattr(net, "set_precision"):
+        net.set_precision(precision)
+    t2i = ncfg["name"] == "uvit_t2i"
     null_label = ncfg["num_classes"] - 1 if ncfg.get("num_classes", -1) > 0 else None
-    sampler = ClassCondSampler(net, front_end=full["front_end"], cfg_scale=full["cfg_scale"], null_label=null_label,
-                               steps=full["sample_steps"], eps=full.get("eps"), use_graph=not args.no_graph)
+    if t2i:   # configs[3]: prompts -> CLIP contexts (sample_t2i_discrete.py:49-53) -> panoptic co-generation
+        from panopticdiffusionmodels_amd.libs.clip import FrozenCLIPEmbedder
+        from panopticdiffusionmodels_amd.sampler import T2ISampler
+        clip = FrozenCLIPEmbedder()
+        with torch.no_grad():   # seeded synthetic ViT-L/14 text weights (no checkpoint offline)
+            g = torch.Generator().manual_seed(5)
+            for k, v in clip.transformer.state_dict().items():
+                if "norm" in k and k.endswith(".weight"):
+                    v.fill_(1.0)
+                elif v.dim() == 2:
+                    v.copy_(torch.randn(v.shape, generator=g) * 0.02)
+                else:
+                    v.zero_()
+        clip = clip.to(dev)
+        sampler = T2ISampler(net, cfg_scale=full["cfg_scale"], steps=full["sample_steps"],
+                             use_graph=not args.no_graph)
+        empty_ids = torch.full((1, 77), CLIP_EOS, dtype=torch.int64)
+        empty_ids[0, 0] = CLIP_BOS
+        empty_ctx = clip.encode_tokens(empty_ids.to(dev))[0]   # the dataset's empty_context (datasets.py:629)
+    else:
+        sampler = ClassCondSampler(net, front_end=full["front_end"], cfg_scale=full["cfg_scale"],
+                                   null_label=null_label, steps=full["sample_steps"], eps=full.get("eps"),
+                                   use_graph=not args.no_graph)
     ae = get_model(None, scale_factor=full.get("scale_factor", 0.18215), seed=1).to(dev) if not args.no_decode else None
 
     # inputs for every (warmup + timed) step, generated per GLOBAL sample index and resident in HBM
@@ -96,7 +124,18 @@ def main():
         idx = [s * world * B + i for i in parallel.shard(world * B, world, rank)]
         z, y = parallel.sample_inputs(idx, zshape, num_classes=1000 if null_label is not None else None)
         zs.append(z.to(dev))
-        ys.append(y.to(dev) if y is not None else None)
+        if t2i:   # synthetic tokenised prompts (BOS, 5..60 body tokens, EOS padding) + mask tokens, per global index
+            ids = torch.full((len(idx), 77), CLIP_EOS, dtype=torch.int64)
+            mts = []
+            for r, i in enumerate(idx):
+                gi = torch.Generator().manual_seed(4321 * 1_000_003 + i)
+                n = int(torch.randint(5, 61, (1,), generator=gi))
+                ids[r, 0] = CLIP_BOS
+                ids[r, 1:1 + n] = torch.randint(0, CLIP_BOS, (n,), generator=gi)
+                mts.append(torch.randn(1, ncfg["num_panoptic_class"], *zshape[1:], generator=gi))
+            ys.append((ids.to(dev), torch.cat(mts).to(dev)))
+        else:
+            ys.append(y.to(dev) if y is not None else None)
 
     from panopticdiffusionmodels_amd import _lib
     prof = _lib.GemmProfiler(net.native(), max_launches=512)
@@ -107,7 +146,11 @@ def main():
         if timed:
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record()
-        z = sampler.sample(zs[s], ys[s])
+        if t2i:
+            ids, mt = ys[s]
+            z, _pred_mask = sampler.sample(zs[s], clip.encode_tokens(ids), empty_ctx, mt)
+        else:
+            z = sampler.sample(zs[s], ys[s])
         if world > 1:
             z = parallel.gather_latents(z)[rank * B:(rank + 1) * B]
         if timed:
@@ -142,15 +185,22 @@ def main():
     # sampled once more eagerly with libpdm's HIP events around every GEMM launch (recorded on the launch stream);
     # the last forward's launches are read back -- the kernels and shapes of the timed steps
     prof.enable()
-    sampler.sample(zs[-1], ys[-1], eager=True)
+    if t2i:
+        ids, mt = ys[-1]
+        T2ISampler(net, cfg_scale=full["cfg_scale"], steps=full["sample_steps"], use_graph=False).sample(
+            zs[-1], clip.encode_tokens(ids), empty_ctx, mt)
+    else:
+        sampler.sample(zs[-1], ys[-1], eager=True)
     prof.disable()
     torch.cuda.synchronize(dev)
-    roof = gemm_roofline(prof, ncfg, 2 * B if sampler.cfg else B, precision)
+    roof = gemm_roofline(prof, ncfg, 2 * B if t2i or sampler.cfg else B, precision,
+                         with_traffic=args.config == "imagenet256_uvit_large" and B == 95)
     samp_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
 
     images = world * B * args.steps
     value = images / elapsed
+    tf_img = TF_PER_IMAGE.get(args.config)
     res = {
         "metric": "images/sec (whole node), ImageNet256 U-ViT-L 50-step DPM-Solver, 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -164,12 +214,18 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16" if precision == "bf16" else "mxfp8-e4m3 (qkv/proj/fc1/fc2) + bf16",
         "data": f"synthetic (seeded random-init {MODEL_NAMES.get(args.config, args.config)} + KL-f8 weights, "
-                "z_T ~ N(0,1), labels U{0..999})",
+                + ("z_T ~ N(0,1), token ids of 5-60-token prompts, mask tokens ~ N(0,1))" if t2i
+                   else "z_T ~ N(0,1), labels U{0..999})"),
         "config": {"workload": f"{args.config}: 50-step DPM-Solver (fast, order 3), CFG {full['cfg_scale']}, "
                                f"{f'+ KL-f8 decode {8 * zshape[-1]}x{8 * zshape[-1]}' if ae is not None else 'no decode'}",
                    "model": MODEL_NAMES.get(args.config, args.config), "per_gpu_batch": B, "global_batch": world * B,
                    "nfe": sampler.nfe, "hip_graph": not args.no_graph, "parallelism": f"dp{world} (batch-sharded)"},
         "roofline": roof,
+        "end_to_end": None if tf_img is None or ae is None else {
+            "algorithmic_tflop_per_image": tf_img, "achieved_tflops": round(value * tf_img, 1),
+            "frac_of_peak": round(value * tf_img * 1e12 / (world * PEAK_BF16), 4) if precision == "bf16" else None,
+            "roofline_images_per_sec": round(world * PEAK_BF16 / (tf_img * 1e12), 1) if precision == "bf16" else None,
+            "note": "whole job: images/s x algorithmic FLOPs per image (SURVEY.md §8d) vs N x the dense bf16 peak"},
         "breakdown_ms_per_step": {"sample_50nfe": round(samp_ms, 2), "decode": round(dec_ms, 2),
                                   "note": "HIP events on the launch stream around each timed step (graph replay)"},
     }
@@ -193,14 +249,17 @@ def measured_traffic():
     return (fam["hbm_bytes_per_launch"] if fam else None), os.path.basename(files[-1])
 
 
-def gemm_roofline(prof, ncfg, rows, precision="bf16"):
+def gemm_roofline(prof, ncfg, rows, precision="bf16", with_traffic=True):
+    """GEMM-family roofline; `traffic` only for the shapes the committed PMC summary was collected on (the
+    default L/2 bench batch), null otherwise."""
     times_ms, flops = prof.read()
     n = len(times_ms)
     tot_t = sum(times_ms) / 1e3
     tot_f = sum(flops)
     achieved = tot_f / tot_t
-    traffic, tsrc = measured_traffic() if precision == "bf16" else (None, None)
-    kernel = "bf16 GEMM family (all U-ViT linear layers: qkv, proj, fc1, fc2, skip_linear)"
+    traffic, tsrc = measured_traffic() if precision == "bf16" and with_traffic else (None, None)
+    kernel = "bf16 GEMM family (all U-ViT linear layers: qkv, proj, fc1, fc2, skip_linear" + \
+        (", context_embed, zero_convs)" if ncfg["name"] == "uvit_t2i" else ")")
     peak = PEAK_BF16
     if precision == "fp8":
         # mixed family: MXFP8 qkv/proj/fc1/fc2, bf16 skip_linear (K = 2D); peak = the FLOP-weighted harmonic mean
@@ -215,7 +274,51 @@ def gemm_roofline(prof, ncfg, rows, precision="bf16"):
             "measured": "HIP events on the launch stream around each GEMM of the last CFG forward of one eager "
                         "sample of the last step's batch, after the timed region",
             "launches_per_forward": n, "avg_launch_ms": round(tot_t / n * 1e3, 4),
-            "flops_per_launch": round(tot_f / n), "flops_per_forward": gemm_flops_per_forward(ncfg, rows)}
+            "flops_per_launch": round(tot_f / n),
+            "flops_per_forward": gemm_flops_per_forward(ncfg, rows) if ncfg["name"] == "uvit" else round(tot_f)}
+
+
+def cpu_model():
+    try:
+        return [ln for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0].split(":", 1)[1].strip()
+    except Exception:
+        return "unknown"
+
+
+def cpu_baseline_t2i(full, ncfg, kw, sd, cores, with_decode):
+    """configs[3] on the host: one full 50-NFE panoptic co-generation of B = 2 images through the oracle's
+    dpm_solver_pp front end with the t2i CFG closure (train_t2i_discrete.py:387-439, 504-546: cond and uncond as
+    two B-row forwards per NFE, mask co-update, enable_mask_opt) + decode; contexts are random (the CLIP encoder,
+    0.13 % of the FLOPs, is left out)."""
+    from oracle import autoencoder_ref, solver_ref, uvit_ref
+    B = 2
+    g = torch.Generator().manual_seed(0)
+    z = torch.randn(B, *full["z_shape"], generator=g)
+    ctx = torch.randn(B, 77, 768, generator=g)
+    empty = torch.randn(77, 768, generator=g)
+    mt = torch.randn(B, ncfg["num_panoptic_class"], *full["z_shape"][1:], generator=g)
+
+    def nnet(x, t, c, m=None):
+        return uvit_ref.uvit_t2i_forward(sd, kw, x, t, c, mask_token=m, enable_panoptic=m is not None)
+    with torch.no_grad():
+        nnet(z, torch.full((B,), 500.0), ctx, mt)   # warm-up
+        fn = solver_ref.cfg_t2i_closure(nnet, ctx, empty, full["cfg_scale"])
+        t0 = time.perf_counter()
+        lat, _ = solver_ref.pp_sample(fn, solver_ref.sd_betas(), z, steps=full["sample_steps"], mask_token=mt,
+                                      enable_mask_opt=True)
+        t_sample = time.perf_counter() - t0
+        t_dec = 0.0
+        if with_decode:
+            dsd = weights.decoder_state_dict(seed=1)
+            t0 = time.perf_counter()
+            autoencoder_ref.decode(dsd, lat)
+            t_dec = time.perf_counter() - t0
+    assert torch.isfinite(lat).all()
+    return {"value": round(B / (t_sample + t_dec), 5), "unit": "images/sec", "cores": cores, "kind": "port",
+            "cpu": cpu_model(),
+            "sample": f"one full 50-NFE panoptic dpm_solver_pp sample of B={B} (CFG {full['cfg_scale']}: cond + "
+                      f"uncond forwards of {B} rows per NFE, mask co-update) = {t_sample:.1f} s, + KL-f8 decode of "
+                      f"{B} images = {t_dec:.1f} s; random contexts (CLIP encoder excluded)"}
 
 
 def cpu_baseline(full, ncfg, with_decode):
@@ -232,6 +335,8 @@ def cpu_baseline(full, ncfg, with_decode):
     kw = dict(ncfg)
     kw.pop("name")
     sd = weights.nnet_state_dict(ncfg, seed=0, init="reference")
+    if ncfg["name"] == "uvit_t2i":
+        return cpu_baseline_t2i(full, ncfg, kw, sd, cores, with_decode)
     B = 2
     g = torch.Generator().manual_seed(0)
     z = torch.randn(B, *full["z_shape"], generator=g)
@@ -266,12 +371,8 @@ def cpu_baseline(full, ncfg, with_decode):
             autoencoder_ref.decode(dsd, lat)
             t_dec = time.perf_counter() - t0
     assert torch.isfinite(lat).all()
-    try:
-        model_name = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":", 1)[1].strip()
-    except Exception:
-        model_name = "unknown"
     return {"value": round(B / (t_sample + t_dec), 5), "unit": "images/sec", "cores": cores, "kind": "port",
-            "cpu": model_name,
+            "cpu": cpu_model(),
             "sample": f"one full {nfe[0]}-NFE {full['front_end']} sample of B={B} images (CFG {full['cfg_scale']}: "
                       f"cond + uncond forwards of {B} rows per NFE) = {t_sample:.1f} s, + KL-f8 decode of {B} "
                       f"images = {t_dec:.1f} s; images/sec = {B} / total"}
