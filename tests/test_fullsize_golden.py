@@ -1,0 +1,145 @@
+"""Full-size parity against the REFERENCE's own outputs (tests/golden/fullsize.npz, made by
+tests/golden/make_fullsize_golden.py with the reference imported): every BASELINE config's forward at B = 2
+and full 50-NFE CFG samples (L/2 through dpm_solver_pytorch, H/2 through dpm_solver_pp, the panoptic t2i with
+the mask co-update).
+
+CPU: the oracle (oracle/uvit_ref.py) vs the reference forwards, rel-L2 <= 1e-5 — the oracle is pinned at full
+size, not only on tiny nets.  GPU: the HIP forward (rel-L2 <= 2e-2) and the fused HIP-graph samplers (final
+latent <= 1e-2, panoptic mask <= 2e-2), SURVEY.md §8c tolerances.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import uvit_ref
+from panopticdiffusionmodels_amd import configs as C
+from panopticdiffusionmodels_amd import weights as W
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FWD = ["cifar10_uvit_small", "imagenet256_uvit_large", "imagenet256_uvit_huge", "imagenet512_uvit_huge",
+       "mscoco_uvit_small"]
+SAMPLE = ["imagenet256_uvit_large", "imagenet256_uvit_huge", "mscoco_uvit_small"]
+
+
+@pytest.fixture(scope="module")
+def fs():
+    return np.load(os.path.join(REPO, "tests", "golden", "fullsize.npz"))
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _checksum(sd):
+    return np.array([float(v.double().sum()) for v in sd.values()] + [float(v.double().abs().sum()) for v in sd.values()])
+
+
+def fwd_inputs(name, B=2, seed=5):
+    """= make_golden._inputs (the fixture stores their checksum)."""
+    cfg = C.get_config(name)
+    n = cfg["nnet"]
+    g = torch.Generator().manual_seed(seed)
+    Cc, H, Wd = cfg["z_shape"]
+    out = {"x": torch.randn(B, Cc, H, Wd, generator=g), "t": torch.rand(B, generator=g) * 998.0 + 1.0}
+    if n["name"] == "uvit" and n.get("num_classes", -1) > 0:
+        y = torch.randint(0, n["num_classes"] - 1, (B,), generator=g)
+        y[-1] = n["num_classes"] - 1
+        out["y"] = y
+    if n["name"] == "uvit_t2i":
+        out["context"] = torch.randn(B, n["num_clip_token"], n["clip_dim"], generator=g)
+        out["mask_token"] = torch.randn(B, n["num_panoptic_class"], H, Wd, generator=g)
+    return out
+
+
+def sample_inputs(name, seed=99):
+    """= make_fullsize_golden.sample_inputs."""
+    full = C.get_config(name)
+    n = full["nnet"]
+    g = torch.Generator().manual_seed(seed)
+    out = {"z": torch.randn(1, *full["z_shape"], generator=g)}
+    if n.get("num_classes", -1) > 0:
+        out["y"] = torch.randint(0, n["num_classes"] - 1, (1,), generator=g)
+    if n["name"] == "uvit_t2i":
+        out["context"] = torch.randn(1, n["num_clip_token"], n["clip_dim"], generator=g)
+        out["empty_context"] = torch.randn(n["num_clip_token"], n["clip_dim"], generator=g)
+        out["mask_token"] = torch.randn(1, n["num_panoptic_class"], *full["z_shape"][1:], generator=g)
+    return out
+
+
+def _sd(name, seed, init):
+    cfg = C.nnet_kwargs(name)
+    return cfg, W.nnet_state_dict(cfg, seed=seed, init=init)
+
+
+@pytest.mark.parametrize("name", FWD)
+def test_oracle_vs_reference_fullsize_forward(fs, name):
+    torch.set_num_threads(min(8, os.cpu_count() or 8))
+    cfg, sd = _sd(name, 3, "random")
+    np.testing.assert_allclose(_checksum(sd), fs[f"fwd/{name}/sd_checksum"], rtol=1e-9)
+    inp = fwd_inputs(name)
+    np.testing.assert_allclose([float(v.double().sum()) for v in inp.values()], fs[f"fwd/{name}/in_checksum"],
+                               rtol=1e-9)
+    kw = dict(cfg)
+    kind = kw.pop("name")
+    with torch.no_grad():
+        if kind == "uvit_t2i":
+            eps, pm = uvit_ref.uvit_t2i_forward(sd, kw, inp["x"], inp["t"], inp["context"],
+                                                mask_token=inp["mask_token"])
+            assert rel(pm, fs[f"fwd/{name}/pred_mask"]) < 1e-5
+        else:
+            eps = uvit_ref.uvit_forward(sd, kw, inp["x"], inp["t"], inp.get("y"))
+    assert rel(eps, fs[f"fwd/{name}/eps"]) < 1e-5
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FWD)
+def test_hip_vs_reference_fullsize_forward(fs, dev, name):
+    from panopticdiffusionmodels_amd.utils import get_nnet
+    cfg, sd = _sd(name, 3, "random")
+    net = get_nnet(**cfg)
+    net.load_state_dict(sd)
+    net = net.to(dev).eval()
+    inp = {k: v.to(dev) for k, v in fwd_inputs(name).items()}
+    with torch.no_grad():
+        if cfg["name"] == "uvit_t2i":
+            eps, pm = net(inp["x"], inp["t"], inp["context"], mask_token=inp["mask_token"])
+            assert rel(pm, fs[f"fwd/{name}/pred_mask"]) < 2e-2
+        else:
+            eps = net(inp["x"], inp["t"], inp.get("y"))
+    assert torch.isfinite(eps).all()
+    assert rel(eps, fs[f"fwd/{name}/eps"]) < 2e-2, rel(eps, fs[f"fwd/{name}/eps"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SAMPLE)
+def test_hip_sampler_vs_reference_fullsize(fs, dev, name):
+    from panopticdiffusionmodels_amd.sampler import ClassCondSampler, T2ISampler
+    from panopticdiffusionmodels_amd.utils import get_nnet
+    full = C.get_config(name)
+    cfg, sd = _sd(name, 0, "reference")
+    np.testing.assert_allclose(_checksum(sd), fs[f"sample/{name}/sd_checksum"], rtol=1e-9)
+    net = get_nnet(**cfg)
+    net.load_state_dict(sd)
+    net = net.to(dev).eval()
+    inp = {k: v.to(dev) for k, v in sample_inputs(name).items()}
+    if cfg["name"] == "uvit_t2i":
+        z, pm = T2ISampler(net, cfg_scale=full["cfg_scale"], steps=50).sample(inp["z"], inp["context"],
+                                                                               inp["empty_context"], inp["mask_token"])
+        assert rel(pm, fs[f"sample/{name}/pred_mask"]) < 2e-2, rel(pm, fs[f"sample/{name}/pred_mask"])
+    else:
+        s = ClassCondSampler(net, front_end=full["front_end"], cfg_scale=full["cfg_scale"],
+                             null_label=cfg["num_classes"] - 1, steps=50, eps=full.get("eps"))
+        z = s.sample(inp["z"], inp["y"])
+    assert torch.isfinite(z).all()
+    assert rel(z, fs[f"sample/{name}/z"]) < 1e-2, rel(z, fs[f"sample/{name}/z"])
