@@ -1385,7 +1385,8 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
   p.raster = g_gemm_raster ? g_gemm_raster : (p.N >= 8 * BN2 ? 8 : 0);
   p.dbg_tile0 = g_gemm_dbg;
   int algo = g_gemm_algo;
-  if (algo == 0) algo = (p.M >= 4096 && p.N >= 256) ? 7 : 1;
+  // batched GEMMs (decoder AttnBlock q k^T and p v, 1024 rows per image at 256^2) count all batches' rows
+  if (algo == 0) algo = ((long long)p.M * (p.batch > 1 ? p.batch : 1) >= 4096 && p.N >= 256) ? 7 : 1;
   // the 256-tile bf16 epilogue stores 16-byte row chunks: needs N, ldo multiples of 8 and an aligned output
   if ((epi == EPI_BF16 || epi == EPI_GELU) && (p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))) algo = 1;
   if (epi == EPI_F32 && (p.N % 8 || p.ldr % 4 || ((uintptr_t)p.out_f32 & 15) ||
