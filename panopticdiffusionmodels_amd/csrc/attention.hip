@@ -397,8 +397,10 @@ __device__ __forceinline__ float xrow_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-template <int DEBUG>
-__global__ __launch_bounds__(256, 2) void attention_v2_kernel(AttentionArgs p, int nqt, int Lp) {
+// NW = waves per workgroup: 4 when two heads fit per CU (L <= 320), else 8 so the single resident head still
+// has two waves per SIMD (t2i image / mask streams, L = 334 / 590)
+template <int DEBUG, int NW>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(AttentionArgs p, int nqt, int Lp) {
   constexpr int DH = 64;
   constexpr float RESCALE_THR = 8.0f;   // deferred rescale (log2 units): P <= 2^8 in bf16, O / l stay fp32
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -412,8 +414,8 @@ __global__ __launch_bounds__(256, 2) void attention_v2_kernel(AttentionArgs p, i
   const bf16* base = p.qkv + (size_t)b * L * p.ldq + h * DH;
   const int g = lane >> 4, col = lane & 15;
 
-  // tiles of this wave: w, w+4, ...; passes of two tiles (the last pass may hold one)
-  const int my_tiles = nqt > wave ? (nqt - wave + 3) / 4 : 0;
+  // tiles of this wave: w, w+NW, ...; passes of two tiles (the last pass may hold one)
+  const int my_tiles = nqt > wave ? (nqt - wave + NW - 1) / NW : 0;
   const int npass = (my_tiles + 1) / 2;
 
   auto qptr = [&](int tile, int ks) {
@@ -427,20 +429,20 @@ __global__ __launch_bounds__(256, 2) void attention_v2_kernel(AttentionArgs p, i
   if (npass > 0 && DEBUG != 2) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int tile = min(wave + 4 * t, nqt - 1);
+      const int tile = min(wave + NW * t, nqt - 1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) q0[t][ks] = gload16_asm(qptr(tile, ks));
     }
   }
   // K / V DMA in 64-key blocks: block c = row groups 8c .. 8c+7 (8 rows x 128 B each); wave w stages groups
-  // 8c + w and 8c + w + 4 of K and of V, so a block is 4 LDS-DMA per wave (the last block may have fewer)
+  // 8c + w (+ 4 with 4 waves) of K and of V (the last block may have fewer)
   const int ngrp = Lp / 8;
   if (DEBUG != 2) {
     const int r8 = lane >> 3, pc = lane & 7;
     for (int grp0 = 0; grp0 < ngrp; grp0 += 8) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int grp = grp0 + wave + 4 * i;
+      for (int i = 0; i < 8 / NW; ++i) {
+        const int grp = grp0 + wave + NW * i;
         if (grp < ngrp) {
           const int row = grp * 8 + r8;
           const int key = row < L ? row : L - 1;
@@ -457,7 +459,7 @@ __global__ __launch_bounds__(256, 2) void attention_v2_kernel(AttentionArgs p, i
   auto ops_after = [&](int c) {
     int n = 0;
     for (int grp0 = (c + 1) * 8; grp0 < ngrp; grp0 += 8)
-      for (int i = 0; i < 2; ++i) n += (grp0 + wave + 4 * i < ngrp) ? 2 : 0;
+      for (int i = 0; i < 8 / NW; ++i) n += (grp0 + wave + NW * i < ngrp) ? 2 : 0;
     return n;
   };
   auto block_ready = [&](int c) {   // pass 0: block c of K/V landed (all waves) before anyone reads it
@@ -597,7 +599,7 @@ __global__ __launch_bounds__(256, 2) void attention_v2_kernel(AttentionArgs p, i
     asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]));
   }
   for (int pass = 0; pass < npass; ++pass) {
-    const int tl[2] = {wave + 8 * pass, wave + 8 * pass + 4};
+    const int tl[2] = {wave + 2 * NW * pass, wave + 2 * NW * pass + NW};
     const bool two = tl[1] < nqt;
     if (pass == 0) {
       if (DEBUG == 0) {
@@ -906,14 +908,24 @@ hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream) {
     const int smem = Lp * 256;
     static bool attr2 = false;
     if (!attr2) {
-      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<1, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<1, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr2 = true;
     }
-    if (algo == 4) hipLaunchKernelGGL(attention_v2_kernel<0>, dim3(p.B * p.H), dim3(256), smem, stream, p, nqt, Lp);
-    else if (algo == 5) hipLaunchKernelGGL(attention_v2_kernel<1>, dim3(p.B * p.H), dim3(256), smem, stream, p, nqt, Lp);
-    else hipLaunchKernelGGL(attention_v2_kernel<2>, dim3(p.B * p.H), dim3(256), smem, stream, p, nqt, Lp);
+    const dim3 grid(p.B * p.H);
+    if (smem <= 80 * 1024) {   // two heads per CU: 4 waves each
+      if (algo == 4) hipLaunchKernelGGL((attention_v2_kernel<0, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
+      else if (algo == 5) hipLaunchKernelGGL((attention_v2_kernel<1, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
+      else hipLaunchKernelGGL((attention_v2_kernel<2, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
+    } else {                   // one head per CU: 8 waves (two per SIMD)
+      if (algo == 4) hipLaunchKernelGGL((attention_v2_kernel<0, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
+      else if (algo == 5) hipLaunchKernelGGL((attention_v2_kernel<1, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
+      else hipLaunchKernelGGL((attention_v2_kernel<2, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
+    }
     return hipGetLastError();
   }
   if (algo == 0 || algo >= 4) algo = 1;
