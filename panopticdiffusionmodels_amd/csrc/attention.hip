@@ -416,7 +416,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
 
   // tiles of this wave: w, w+NW, ...; passes of two tiles (the last pass may hold one)
   const int my_tiles = nqt > wave ? (nqt - wave + NW - 1) / NW : 0;
-  const int npass = (my_tiles + 1) / 2;
+  // passes of two tiles; an odd count folds its last tile into the final pass (three tiles) instead of a
+  // one-tile pass of its own (L = 258: the ragged 17th tile of wave 0)
+  const int npass = my_tiles == 1 ? 1 : my_tiles / 2;
 
   auto qptr = [&](int tile, int ks) {
     int q = tile * 16 + col;
@@ -425,10 +427,10 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
   };
   // Q fragments of the first pass (B operand): lane holds Q[q = tile*16 + col][d = ks*32 + g*8 .. +8], loaded
   // by inline asm ahead of the K/V DMA (a compiler-visible load would make hipcc drain the DMA queue)
-  i32x4 q0[2][2];
+  i32x4 q0[3][2];
   if (npass > 0 && DEBUG != 2) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < 3; ++t) {
       const int tile = min(wave + NW * t, nqt - 1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) q0[t][ks] = gload16_asm(qptr(tile, ks));
@@ -473,7 +475,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
   const int nfull = L / 64, nch = (L + 63) / 64;
 
   // one pass over all keys for NT query tiles (qf), writing the normalised rows of tiles tl[0..NT)
-  auto run_pass = [&](auto ntc, const bf16x8 (&qf)[2][2], const int (&tl)[2], bool first) {
+  auto run_pass = [&](auto ntc, const bf16x8 (&qf)[3][2], const int (&tl)[3], bool first) {
     constexpr int NT = decltype(ntc)::value;
     float m_run[NT], l_run[NT];
     f32x4 acc[NT][4];
@@ -594,33 +596,34 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
     for (int c = 0; c < nch; ++c) block_ready(c);
     return;
   }
-  bf16x8 qf[2][2];
+  bf16x8 qf[3][2];
   if (DEBUG != 2) {
-    asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]));
+    asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]), "+v"(q0[2][0]), "+v"(q0[2][1]));
   }
   for (int pass = 0; pass < npass; ++pass) {
-    const int tl[2] = {wave + 2 * NW * pass, wave + 2 * NW * pass + NW};
-    const bool two = tl[1] < nqt;
+    const int tl[3] = {wave + 2 * NW * pass, wave + 2 * NW * pass + NW, wave + 2 * NW * pass + 2 * NW};
+    const int nt = my_tiles == 1 ? 1 : (pass == npass - 1 && (my_tiles & 1) ? 3 : 2);
     if (pass == 0) {
       if (DEBUG == 0) {
         // Q (the oldest loads) retired together with block 0; "+v" keeps every consumer below the wait
         wait_vmcnt_dyn(ops_after(0));
-        asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]));
+        asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]), "+v"(q0[2][0]), "+v"(q0[2][1]));
       } else if (DEBUG == 1) {
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]));
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]), "+v"(q0[2][0]),
+                     "+v"(q0[2][1]));
       }
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 3; ++t)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) qf[t][ks] = __builtin_bit_cast(bf16x8, q0[t][ks]);
     } else {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        qf[0][ks] = *reinterpret_cast<const bf16x8*>(qptr(tl[0], ks));
-        qf[1][ks] = *reinterpret_cast<const bf16x8*>(qptr(two ? tl[1] : tl[0], ks));
-      }
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) qf[t][ks] = *reinterpret_cast<const bf16x8*>(qptr(t < nt ? tl[t] : tl[0], ks));
     }
-    if (two) run_pass(std::integral_constant<int, 2>{}, qf, tl, pass == 0);
+    if (nt == 3) run_pass(std::integral_constant<int, 3>{}, qf, tl, pass == 0);
+    else if (nt == 2) run_pass(std::integral_constant<int, 2>{}, qf, tl, pass == 0);
     else run_pass(std::integral_constant<int, 1>{}, qf, tl, pass == 0);
   }
 }
