@@ -271,7 +271,8 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
           if (p.act) {
             v[0] = gelu_quick(v[0]); v[1] = gelu_quick(v[1]); v[2] = gelu_quick(v[2]); v[3] = gelu_quick(v[3]);
           } else {
-            v[0] = gelu_erf(v[0]); v[1] = gelu_erf(v[1]); v[2] = gelu_erf(v[2]); v[3] = gelu_erf(v[3]);
+            const f32x2 lo = gelu_erf2(f32x2{v[0], v[1]}), hi = gelu_erf2(f32x2{v[2], v[3]});
+            v = f32x4{lo[0], lo[1], hi[0], hi[1]};
           }
         }
         const int off = ml * 512 + ((((nl >> 3) ^ (ml & 31)) << 4) | ((nl & 4) << 1));

@@ -44,6 +44,29 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return fmaf(-0.5f * a, r, fmaxf(x, 0.0f));
 }
 
+// The same GELU on two values at once, written on 2-wide vectors so the polynomial, the squarings and the final
+// FMA issue as packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes' work per VALU cycle); only the
+// reciprocals stay scalar.  max(x, 0) is folded as (x + |x|) / 2 (exact), so the tail is
+// GELU = 0.5 (x + |x| - |x| p^-16): one packed add, FMA and multiply, no scalar max / NaN canonicalisation
+// (within 1 ulp of gelu_erf).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 a = __builtin_elementwise_abs(x);
+  const f32x2 z = a * 0.70710678118654752440f;
+  f32x2 p = __builtin_elementwise_fma(z, f32x2(4.30638e-5f), f32x2(2.765672e-4f));
+  p = __builtin_elementwise_fma(p, z, f32x2(1.520143e-4f));
+  p = __builtin_elementwise_fma(p, z, f32x2(9.2705272e-3f));
+  p = __builtin_elementwise_fma(p, z, f32x2(4.22820123e-2f));
+  p = __builtin_elementwise_fma(p, z, f32x2(7.05230784e-2f));
+  p = __builtin_elementwise_fma(p, z, f32x2(1.0f));
+  f32x2 r = {__builtin_amdgcn_rcpf(p[0]), __builtin_amdgcn_rcpf(p[1])};
+  r *= r;
+  r *= r;
+  r *= r;
+  r *= r;
+  return __builtin_elementwise_fma(-a, r, x + a) * 0.5f;
+}
+
 // quick GELU (transformers QuickGELUActivation, CLIP text encoder): x * sigmoid(1.702 x)
 __device__ __forceinline__ float gelu_quick(float x) { return x / (1.0f + __expf(-1.702f * x)); }
 __device__ __forceinline__ float gelu_act(int act, float x) { return act ? gelu_quick(x) : gelu_erf(x); }
