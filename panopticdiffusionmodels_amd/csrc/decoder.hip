@@ -102,37 +102,51 @@ __global__ __launch_bounds__(256) void gn_final_kernel(const double* part, int n
   stats[i * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
-// y = [swish]((x - mean) * rstd * gamma + beta), NHWC, 4 channels per thread, bf16 out
+// y = [swish]((x - mean) * rstd * gamma + beta), NHWC, bf16 out.  Grid (gx, B): a block stays in one image and
+// every thread keeps one channel octet q (C <= 2048, C % 8 == 0) for all its pixels, so the per-channel affine
+// a = rstd * gamma, b = beta - mean * a is folded once into registers and the pixel loop is two 16-byte loads
+// (fp32; one for bf16), one FMA + swish per element and one 16-byte store, 32-bit indexing only.  (The first
+// version decoded (image, pixel, channel) from a flat 64-bit index per element and reloaded stats, gamma and
+// beta per element: ~40 % of HBM bandwidth.)  swish = u / (1 + 2^(-u log2 e)) with the hardware exp2 and
+// reciprocal (u -> -inf gives -0, no NaN).
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const T* x, const float* stats, const float* gamma,
-                                                       const float* beta, bf16* y, long long P, int C, int swish,
-                                                       int B) {
-  const int nq = C / 4;
-  const long long total = (long long)B * P * nq;
-  const int cpg = C / 32;
-  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-    const int q = (int)(e % nq);
-    const long long pix = e / nq;
-    const int b = (int)(pix / P);
-    const int c = q * 4;
-    float v[4];
-    if constexpr (sizeof(T) == 4) {
-      const f32x4 t = *reinterpret_cast<const f32x4*>(x + pix * C + c);
-      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
-    } else {
-      const bf16x4 t = *reinterpret_cast<const bf16x4*>(x + pix * C + c);
-      v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
-    }
-    bf16x4 o;
+                                                       const float* beta, bf16* y, int P, int C, int swish) {
+  const int no = C >> 3, planes = 256 / no, q = threadIdx.x % no, plane = threadIdx.x / no;
+  if (plane >= planes) return;
+  const int b = blockIdx.y, c = q * 8, cpg = C / 32;
+  float a[8], o[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int g = (c + j) / cpg;   // cpg may be 2 or 6: a quad can straddle two groups
-      const float mean = stats[(b * 32 + g) * 2], rstd = stats[(b * 32 + g) * 2 + 1];
-      float u = (v[j] - mean) * rstd * gamma[c + j] + beta[c + j];
-      if (swish) u = u / (1.0f + __expf(-u));
-      o[j] = (bf16)u;
+  for (int j = 0; j < 8; ++j) {
+    const int g = (c + j) / cpg;   // cpg may be 2 or 6: an octet can straddle groups
+    const float mean = stats[(b * 32 + g) * 2], rstd = stats[(b * 32 + g) * 2 + 1];
+    a[j] = rstd * gamma[c + j];
+    o[j] = fmaf(-mean, a[j], beta[c + j]);
+  }
+  const T* xb = x + (size_t)b * P * C + c;
+  bf16* yb = y + (size_t)b * P * C + c;
+  const int step = gridDim.x * planes;
+#pragma unroll 2
+  for (int pi = blockIdx.x * planes + plane; pi < P; pi += step) {
+    float v[8];
+    if constexpr (sizeof(T) == 4) {
+      const f32x4 t0 = *reinterpret_cast<const f32x4*>(xb + (size_t)pi * C);
+      const f32x4 t1 = *reinterpret_cast<const f32x4*>(xb + (size_t)pi * C + 4);
+      v[0] = t0[0]; v[1] = t0[1]; v[2] = t0[2]; v[3] = t0[3];
+      v[4] = t1[0]; v[5] = t1[1]; v[6] = t1[2]; v[7] = t1[3];
+    } else {
+      const bf16x8 t = *reinterpret_cast<const bf16x8*>(xb + (size_t)pi * C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)t[j];
     }
-    *reinterpret_cast<bf16x4*>(y + pix * C + c) = o;
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float u = fmaf(v[j], a[j], o[j]);
+      if (swish) u *= __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u * -1.4426950408889634f));
+      r[j] = (bf16)u;
+    }
+    *reinterpret_cast<bf16x8*>(yb + (size_t)pi * C) = r;
   }
 }
 
@@ -299,11 +313,6 @@ __global__ __launch_bounds__(256) void conv_out8_kernel(const bf16* g, int B, in
   }
 }
 
-inline int gridn(long long n) {
-  long long g = (n + 255) / 256;
-  return (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
-}
-
 }  // namespace
 }  // namespace pdm
 
@@ -435,9 +444,11 @@ int groupnorm(const DCtx& c, const T* x, int B, int P, int C, const std::string&
   hipLaunchKernelGGL(pdm::gn_partial_kernel<T>, dim3(nchunk, B), dim3(256), 0, c.s, x, P, C, nchunk, pix, c.w->part);
   hipLaunchKernelGGL(pdm::gn_final_kernel, dim3((B * 32 + 3) / 4), dim3(256), 0, c.s, c.w->part, nchunk,
                      (double)P * (C / 32), 1e-6f, c.w->stats, B);
-  const long long n = (long long)B * P * (C / 4);
-  hipLaunchKernelGGL(pdm::gn_apply_kernel<T>, dim3(pdm::gridn(n)), dim3(256), 0, c.s, x, c.w->stats,
-                     c.d->f(norm + ".weight"), c.d->f(norm + ".bias"), y, (long long)P, C, swish ? 1 : 0, B);
+  if (C % 8 || C > 2048) return dfail(PDM_ERR_ARG, "decoder: GroupNorm needs C % 8 == 0 and C <= 2048");
+  const int planes = 256 / (C / 8);
+  const int gx = std::max(1, std::min((P + planes - 1) / planes, 2048 / B + 1));   // >= ~2048 blocks in flight
+  hipLaunchKernelGGL(pdm::gn_apply_kernel<T>, dim3(gx, B), dim3(256), 0, c.s, x, c.w->stats,
+                     c.d->f(norm + ".weight"), c.d->f(norm + ".bias"), y, P, C, swish ? 1 : 0);
   D_HIP(hipGetLastError());
   return PDM_OK;
 }
