@@ -327,8 +327,24 @@ __global__ __launch_bounds__(256) void rowcopy_kernel(float* dst, int ldd, const
   for (int j = threadIdx.x; j < (D >> 2); j += 256) d[j] = s[j];
 }
 
+// fp32 -> bf16 (round to nearest even).  Eight elements per thread when x and y are 16-B aligned: two
+// 16-byte loads and one 16-byte store (the scalar 4-B load / 2-B store form ran at ~45 % of HBM bandwidth);
+// the scalar loop covers the n % 8 tail and unaligned views.
 __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* x, bf16* y, long long n) {
-  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) y[e] = (bf16)x[e];
+  const long long stride = (long long)gridDim.x * 256;
+  long long done = 0;
+  if ((((uintptr_t)x | (uintptr_t)y) & 15) == 0) {
+    const long long n8 = n >> 3;
+    for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n8; e += stride) {
+      const f32x4 a = reinterpret_cast<const f32x4*>(x)[2 * e], b = reinterpret_cast<const f32x4*>(x)[2 * e + 1];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { o[j] = (bf16)a[j]; o[4 + j] = (bf16)b[j]; }
+      reinterpret_cast<bf16x8*>(y)[e] = o;
+    }
+    done = n8 << 3;
+  }
+  for (long long e = done + blockIdx.x * 256ll + threadIdx.x; e < n; e += stride) y[e] = (bf16)x[e];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -467,7 +483,7 @@ hipError_t lincomb_launch(float* out, int n_terms, const float* const* T, const 
 }
 
 hipError_t cast_bf16_launch(const float* x, bf16* y, long long n, hipStream_t stream) {
-  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, stream, x, y, n);
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for((n + 7) / 8)), dim3(256), 0, stream, x, y, n);
   return hipGetLastError();
 }
 

@@ -35,3 +35,24 @@ def test_masks_to_ids_rgb(dev):
     ref_ids = utils_ref.bits2int(bits.numpy() > 0)[:, 0]
     np.testing.assert_array_equal(ids.cpu().numpy(), ref_ids)
     np.testing.assert_array_equal(rgb.cpu().numpy(), utils_ref.color_map(ref_ids, cmap.numpy()))
+
+
+@pytest.mark.parametrize("n,off_x,off_y", [(0, 0, 0), (7, 0, 0), (8, 0, 0), (1 << 20, 0, 0), (1_000_003, 0, 0),
+                                           (4099, 1, 0), (4099, 0, 3), (4104, 4, 8)])
+def test_f32_to_bf16_cast(dev, n, off_x, off_y):
+    """pdm_f32_to_bf16 (the decoder / t2i context cast): vector body + scalar tail + unaligned views, bit-exact vs
+    torch's round-to-nearest-even, inf / nan / denormals included."""
+    from panopticdiffusionmodels_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator(device=dev).manual_seed(n)
+    xs = torch.randn(n + off_x, device=dev, generator=g) * 100
+    if n > 16:
+        xs[off_x:off_x + 4] = torch.tensor([float("inf"), -float("inf"), 1e-40, -0.0], device=dev)
+    x = xs[off_x:]
+    ys = torch.full((n + off_y,), 7.0, device=dev, dtype=torch.bfloat16)
+    y = ys[off_y:]
+    rc = lib.pdm_f32_to_bf16(x.data_ptr(), y.data_ptr(), n, _lib.stream_ptr(dev))
+    assert rc == 0, lib.pdm_last_error()
+    torch.cuda.synchronize(dev)
+    assert torch.equal(y.view(torch.int16), x.bfloat16().view(torch.int16))
+    assert torch.equal(ys[:off_y], torch.full((off_y,), 7.0, device=dev, dtype=torch.bfloat16))
