@@ -187,7 +187,7 @@ int pdm_layernorm(const float* x, int ldx, const float* gamma, const float* beta
 /* Attention core (libs/uvit.py:66-92 minus the two Linears): packed qkv bf16 -> bf16 */
 int pdm_attention(const void* qkv, int ldq, void* out, int ldo, int B, int L, int H, int Dh, float scale,
                   void* stream);
-/* fp32 -> bf16 conversion */
+/* fp32 -> bf16 conversion (round to nearest even); n == 0 is a no-op (null pointers allowed) */
 int pdm_f32_to_bf16(const float* x, void* y, long long n, void* stream);
 /* MXFP8 quantisation of rows x [rows][ldx] (dtype PDM_F32 or PDM_BF16, K % 32 == 0) -> e4m3 q [rows][ldq] and
  * E8M0 scale dwords s [ceil(K/128)][s_ld >= rows]: exponent ceil(log2(amax/448)) per 32 columns, RNE data (the

@@ -966,6 +966,7 @@ int pdm_mx_quantize(const void* x, int dtype, int ldx, int rows, int K, void* q,
 }
 
 int pdm_f32_to_bf16(const float* x, void* y, long long n, void* stream) {
+  if (n == 0) return PDM_OK;   // empty tensors may carry null data pointers
   if (!x || !y || n < 0) return fail(PDM_ERR_ARG, "pdm_f32_to_bf16: bad argument");
   PDM_HIP(pdm::cast_bf16_launch(x, (bf16*)y, n, (hipStream_t)stream));
   return PDM_OK;
