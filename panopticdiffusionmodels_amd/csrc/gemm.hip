@@ -179,6 +179,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p, int tiles
 constexpr int BM2 = 256, BN2 = 256;
 constexpr int EPI_LDS = 128 * 1024;             // the 256-tile epilogue's staging area; LN row stats follow it
 constexpr int EPI_LDS_EXTRA = 256 * 8;
+constexpr int COL_LDS = EPI_LDS + EPI_LDS_EXTRA;   // gemm8d: the tile's bias [256] and LN colsum [256] (fp32)
+constexpr int COL_LDS_BYTES = 2 * 256 * 4;
 
 template <int BK>
 __device__ __forceinline__ int swz_off(int row, int chunk) {
@@ -219,13 +221,23 @@ __device__ __forceinline__ void frag_pos(int f, int lane, int wm, int wn, int& m
 //    2 x 16-byte residual loads, 2 x 16-byte stores and one 16-byte bf16 copy store per row chunk.
 template <int EPI, int MAP>
 __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc)[32], char* smem, int m0, int n0,
-                                            int tid, int lane, int wm, int wn, bool ln_ready = false) {
+                                            int tid, int lane, int wm, int wn, bool ln_ready = false,
+                                            bool cols_ready = false) {
   // bias of the lane's 4 column groups, loaded up front with one wave-uniform branch (columns past N read a
   // clamped address and are never stored)
   f32x4 bv[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) bv[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (EPI != EPI_F32 && p.bias) {
+  // cols_ready: the kernel staged the tile's bias / colsum (zeros past N or when absent) at COL_LDS in its prologue
+  const float* lcol = reinterpret_cast<const float*>(smem + COL_LDS);
+  if (EPI != EPI_F32 && cols_ready) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      int ml, nl;
+      frag_pos<MAP>(MAP == 0 ? g * 8 : (g >> 1) * 8 + (g & 1) * 4, lane, wm, wn, ml, nl);
+      bv[g] = *reinterpret_cast<const f32x4*>(lcol + nl);
+    }
+  } else if (EPI != EPI_F32 && p.bias) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       int ml, nl;
@@ -245,7 +257,8 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
     for (int g = 0; g < 4; ++g) {
       int ml, nl;
       frag_pos<MAP>(MAP == 0 ? g * 8 : (g >> 1) * 8 + (g & 1) * 4, lane, wm, wn, ml, nl);
-      cs[g] = *reinterpret_cast<const f32x4*>(p.ln_colsum + min(n0 + nl, p.N - 4));
+      cs[g] = cols_ready ? *reinterpret_cast<const f32x4*>(lcol + 256 + nl)
+                         : *reinterpret_cast<const f32x4*>(p.ln_colsum + min(n0 + nl, p.N - 4));
     }
     if (tid < 256 && !ln_ready) {   // ln_ready: the kernel merged them into lnrow during its prologue
       const int m = min(m0 + tid, p.M - 1);
@@ -353,7 +366,10 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
     if (m < p.M && n < p.N) mx_store8(p.out_fp8, p.ldo8, p.out_scale, p.out_scale_ld, m, n, q, e8, (tid & 3) == 0);
   };
   f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
-  if (p.bias) {
+  if (cols_ready) {
+    b0 = *reinterpret_cast<const f32x4*>(lcol + (tid & 31) * 8);
+    b1 = *reinterpret_cast<const f32x4*>(lcol + (tid & 31) * 8 + 4);
+  } else if (p.bias) {
     const int n = min(n0 + (tid & 31) * 8, p.N - 8 >= 0 ? p.N - 8 : 0);
     b0 = *reinterpret_cast<const f32x4*>(p.bias + n);
     if (n + 4 < p.N) b1 = *reinterpret_cast<const f32x4*>(p.bias + n + 4);
@@ -882,7 +898,19 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
 #pragma unroll
     for (int t = 0; t < 8; ++t) lst[t] = t < p.ln_ld ? st[t] : make_float2(0.f, 0.f);
   }
+  // the same for the tile's bias and LN column sums (waves 4-7, one column each) -> COL_LDS, so no epilogue
+  // opens with a global-load round trip
+  float cb = 0.f, cc = 0.f;
+  if (tid >= 256) {
+    const int n = n0 + tid - 256;
+    if (p.bias && n < p.N) cb = p.bias[n];
+    if (ln_pre && n < p.N) cc = p.ln_colsum[n];
+  }
   auto ln_prologue = [&]() {
+    if (tid >= 256) {
+      reinterpret_cast<float*>(smem + COL_LDS)[tid - 256] = cb;
+      reinterpret_cast<float*>(smem + COL_LDS)[tid] = cc;   // colsum at +256
+    }
     if (ln_pre && tid < 256) {   // ln_merge's arithmetic, in the same order, on the registers
       float sum = 0.f;
 #pragma unroll
@@ -1053,7 +1081,7 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
   }
   if (wave < 4) bar_raw();                             // rejoin the stagger
 
-  epilogue256<EPI, 1>(p, acc, smem, m0, n0, tid, lane, wm, wn, ln_pre);
+  epilogue256<EPI, 1>(p, acc, smem, m0, n0, tid, lane, wm, wn, ln_pre, true);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1359,7 +1387,7 @@ static hipError_t launch8p(const GemmArgs& p, int epi, hipStream_t stream) {
 
 template <int CONV, int SCHED>
 static hipError_t launch8d(const GemmArgs& p, int epi, hipStream_t stream) {
-  constexpr int SMEM = 2 * 4 * 128 * 128 + EPI_LDS_EXTRA;   // 128 KiB ring + LN row stats
+  constexpr int SMEM = 2 * 4 * 128 * 128 + EPI_LDS_EXTRA + COL_LDS_BYTES;   // ring + LN rows + bias / colsum
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm8d_kernel<EPI_BF16, CONV, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
