@@ -40,6 +40,7 @@ MODEL_NAMES = {"imagenet256_uvit_large": "U-ViT-L/2", "imagenet256_uvit_huge": "
 TF_PER_IMAGE = {"imagenet256_uvit_large": 15.913, "imagenet256_uvit_huge": 27.261, "imagenet512_uvit_huge": 29.160,
                 "mscoco_uvit_small": 10.221 + 0.0131, "cifar10_uvit_small": 1.220}
 CLIP_BOS, CLIP_EOS = 49406, 49407
+FP8_SET = {"fp8": "qkv/proj/fc2", "fp8-all": "qkv/proj/fc1/fc2"}   # libs/uvit.py UViT.set_precision
 
 
 def parse():
@@ -53,6 +54,8 @@ def parse():
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--precision", choices=["bf16", "fp8", "fp8-all"], default=None,
+                    help="override the config's block-Linear precision (configs[4] default: fp8)")
     return ap.parse_args()
 
 
@@ -71,11 +74,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
+        if world == 1:
             raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one process per GPU)")
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}: launch one process per GPU with "
+                         f"--nproc-per-node equal to --gpus")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # any launch through torch.distributed.run (RANK/MASTER_ADDR set) joins an RCCL group, world size 1 included,
+    # so the barrier / all_reduce(MAX) / all-gather legs run exactly as at N > 1
+    distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ
+    if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
     full = configs.get_config(args.config)
@@ -86,7 +94,7 @@ def main():
     net = get_nnet(**ncfg).to(dev).eval()
     net.load_state_dict(sd)
     del sd
-    precision = full.get("precision", "bf16")   # configs[4]: MXFP8 block Linears (UViT.set_precision)
+    precision = args.precision or full.get("precision", "bf16")   # configs[4]: MXFP8 (UViT.set_precision)
     if hasattr(net, "set_precision"):
         net.set_precision(precision)
     t2i = ncfg["name"] == "uvit_t2i"
@@ -151,7 +159,7 @@ def main():
             z, _pred_mask = sampler.sample(zs[s], clip.encode_tokens(ids), empty_ctx, mt)
         else:
             z = sampler.sample(zs[s], ys[s])
-        if world > 1:
+        if distributed:
             z = parallel.gather_latents(z)[rank * B:(rank + 1) * B]
         if timed:
             e[1].record()
@@ -164,18 +172,18 @@ def main():
     for s in range(args.warmup):
         one_step(s)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.warmup, nsteps):
         out = one_step(s, timed=True)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -202,7 +210,7 @@ def main():
     value = images / elapsed
     tf_img = TF_PER_IMAGE.get(args.config)
     res = {
-        "metric": "images/sec (whole node), ImageNet256 U-ViT-L 50-step DPM-Solver, 1/2/4/8 GPU",
+        "metric": metric_name(args.config, zshape, ae is not None),
         "value": round(value, 3),
         "unit": "images/sec",
         "n_gpus": world,
@@ -212,7 +220,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if precision == "bf16" else "mxfp8-e4m3 (qkv/proj/fc1/fc2) + bf16",
+        "dtype": "bf16" if precision == "bf16" else f"mxfp8-e4m3 ({FP8_SET[precision]}) + bf16",
         "data": f"synthetic (seeded random-init {MODEL_NAMES.get(args.config, args.config)} + KL-f8 weights, "
                 + ("z_T ~ N(0,1), token ids of 5-60-token prompts, mask tokens ~ N(0,1))" if t2i
                    else "z_T ~ N(0,1), labels U{0..999})"),
@@ -233,8 +241,20 @@ def main():
         res["cpu_baseline"] = cpu_baseline(full, ncfg, ae is not None)
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
+
+
+def metric_name(config, zshape, with_decode):
+    """BASELINE.json's metric for the headline config; the same wording with the model / resolution of the
+    other configs (their lines are extra evidence, not the headline)."""
+    if config == "imagenet256_uvit_large" and with_decode:
+        return "images/sec (whole node), ImageNet256 U-ViT-L 50-step DPM-Solver, 1/2/4/8 GPU"
+    data = {"imagenet256_uvit_huge": "ImageNet256", "imagenet512_uvit_huge": "ImageNet512",
+            "mscoco_uvit_small": "MSCOCO256 t2i + panoptic", "cifar10_uvit_small": "CIFAR10"}.get(config, config)
+    res = 8 * zshape[-1] if config != "cifar10_uvit_small" else zshape[-1]
+    return (f"images/sec (whole node), {data} {MODEL_NAMES.get(config, config)} 50-step DPM-Solver"
+            f"{f', {res}x{res} decode' if with_decode else ', latents only (no decode)'}")
 
 
 def measured_traffic():
@@ -257,16 +277,21 @@ def gemm_roofline(prof, ncfg, rows, precision="bf16", with_traffic=True):
     tot_t = sum(times_ms) / 1e3
     tot_f = sum(flops)
     achieved = tot_f / tot_t
-    traffic, tsrc = measured_traffic() if precision == "bf16" and with_traffic else (None, None)
+    traffic, tsrc = measured_traffic() if precision == "bf16" and with_traffic else (None, None)  # noqa
     kernel = "bf16 GEMM family (all U-ViT linear layers: qkv, proj, fc1, fc2, skip_linear" + \
         (", context_embed, zero_convs)" if ncfg["name"] == "uvit_t2i" else ")")
     peak = PEAK_BF16
-    if precision == "fp8":
-        # mixed family: MXFP8 qkv/proj/fc1/fc2, bf16 skip_linear (K = 2D); peak = the FLOP-weighted harmonic mean
+    if precision != "bf16":
+        # mixed family: MXFP8 qkv/proj/fc2 (+ fc1 for 'fp8-all'), bf16 skip_linear (K = 2D) and fc1 ('fp8');
+        # peak = the FLOP-weighted harmonic mean of the two dense peaks
         D, L = ncfg["embed_dim"], (ncfg["img_size"] // ncfg["patch_size"]) ** 2 + 2
-        f_skip = (ncfg["depth"] // 2) * 2.0 * rows * L * D * 2 * D
-        peak = tot_f / ((tot_f - f_skip) / PEAK_FP8 + f_skip / PEAK_BF16)
-        kernel = "GEMM family: MXFP8 qkv/proj/fc1/fc2 + bf16 skip_linear (FLOP-weighted fp8/bf16 peak)"
+        Hd = int(D * ncfg.get("mlp_ratio", 4))
+        f_bf16 = (ncfg["depth"] // 2) * 2.0 * rows * L * D * 2 * D
+        if precision == "fp8":
+            f_bf16 += (ncfg["depth"] + 1) * 2.0 * rows * L * D * Hd
+        peak = tot_f / ((tot_f - f_bf16) / PEAK_FP8 + f_bf16 / PEAK_BF16)
+        kernel = (f"GEMM family: MXFP8 {FP8_SET[precision]} + bf16 skip_linear"
+                  f"{' and fc1' if precision == 'fp8' else ''} (FLOP-weighted fp8/bf16 peak)")
     return {"bound": "mfma", "kernel": kernel,
             "achieved": round(achieved / 1e12, 1), "peak": round(peak / 1e12, 1), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic,

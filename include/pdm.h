@@ -70,8 +70,14 @@ typedef struct pdm_uvit_cfg {
    * embed_dim and mlp hidden multiples of 128).  attn.qkv / attn.proj / mlp.fc1 / mlp.fc2 weights are then
    * PDM_FP8 [out][in] with a "<key>_scale" PDM_E8M0 [in/128][out] companion (qkv / fc1: quantised after the
    * norm fold); every activation feeding them is MXFP8, written by the epilogue that produces it.  Everything
-   * else (skip_linear, whose output replaces the residual stream, attention, heads) stays as in the bf16 path. */
+   * else (skip_linear, whose output replaces the residual stream, attention, heads) stays as in the bf16 path.
+   * The residual-stream operands of the LayerNorm-fused Linears are MXFP8 of x minus its 256-column group means
+   * and those Linears also take "<key minus .weight>.ln_gcol" bf16 [out][16] (pdm_gemm_args.ln_gcol). */
   int fp8;
+  /* with fp8: which block Linears are MXFP8, bit 0 attn.qkv, 1 attn.proj, 2 mlp.fc1, 3 mlp.fc2; 0 = all four.
+   * Supported: 0 / 0xF, and 0xB (mlp.fc1 in bf16: the forward error of the H/4 net drops from 6.9e-2 to
+   * 5.0e-2 rel-L2, tools/fp8_ablation.py).  A bf16 Linear's weight is registered as in the bf16 path. */
+  int fp8_linears;
 } pdm_uvit_cfg;
 
 /* replaces utils.get_nnet (utils.py:291-299) + UViT.__init__ (libs/uvit.py:139-195) */
@@ -170,6 +176,13 @@ typedef struct pdm_gemm_args {
   const unsigned* w_scale; int w_scale_ld;
   void* out_fp8; int ldo8;
   unsigned* out_scale; int out_scale_ld;
+  /* group-centred MXFP8 LayerNorm operands.  mx_center (fp32 epilogue with stats_out and out_fp8): the MXFP8
+   * copy holds x - mu_t, mu_t = stats_out's sum / width of the row's 256-column group t.  ln_gcol (fp8
+   * consumer with ln_stats): A holds such a centred copy; ln_gcol [N][16] bf16 = per column n the group sums
+   * c_t[n] = sum_{k in group t} W[n][k] of the dequantised weight as bf16 pairs (hi at [t], lo at [8 + t]);
+   *   out = rstd * (A W^T + sum_t (mu_t - mean) c_t) + bias   (ln_colsum then unused) */
+  int mx_center;
+  const void* ln_gcol;
 } pdm_gemm_args;
 int pdm_gemm(const pdm_gemm_args* a, int epi, void* stream);
 /* Implicit-GEMM conv3x3 (stride 1, pad 1) on NHWC bf16 input [B, H>>up, W>>up, Cin] (up = 1: the nearest-x2

@@ -20,7 +20,7 @@ class PdmUvitCfg(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "img_size", "patch_size", "in_chans", "embed_dim", "depth", "num_heads", "mlp_hidden", "num_classes",
         "conv", "skip", "qkv_bias", "mlp_time_embed", "t2i", "clip_dim", "num_clip_token", "separate",
-        "enable_panoptic", "num_panoptic_class", "fp8")]
+        "enable_panoptic", "num_panoptic_class", "fp8", "fp8_linears")]
 
 
 class PdmDecoderCfg(ctypes.Structure):
@@ -57,6 +57,7 @@ class PdmGemmArgs(ctypes.Structure):
         ("a_scale", ctypes.c_void_p), ("a_scale_ld", ctypes.c_int), ("w_scale", ctypes.c_void_p),
         ("w_scale_ld", ctypes.c_int), ("out_fp8", ctypes.c_void_p), ("ldo8", ctypes.c_int),
         ("out_scale", ctypes.c_void_p), ("out_scale_ld", ctypes.c_int),
+        ("mx_center", ctypes.c_int), ("ln_gcol", ctypes.c_void_p),
     ]
 
 
@@ -284,7 +285,8 @@ def mx_quantize_gpu(x):
 
 
 def gemm_ex(epi, a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=None, accumulate=False,
-            ln_stats=None, ln_colsum=None, stats_out=None, out_fp8=None, out_scale=None, eps=1e-5):
+            ln_stats=None, ln_colsum=None, stats_out=None, out_fp8=None, out_scale=None, eps=1e-5,
+            mx_center=False, ln_gcol=None):
     """pdm_gemm with every option (include/pdm.h pdm_gemm_args).  a / w are bf16, or float8_e4m3fn with their
     scale dword arrays (MXFP8)."""
     lib = load()
@@ -312,7 +314,22 @@ def gemm_ex(epi, a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=
     if out_fp8 is not None:
         g.out_fp8, g.ldo8 = out_fp8.data_ptr(), out_fp8.stride(0)
         g.out_scale, g.out_scale_ld = out_scale.data_ptr(), out_scale.shape[1]
+    g.mx_center = int(mx_center)
+    g.ln_gcol = ln_gcol.data_ptr() if ln_gcol is not None else None
     check(lib.pdm_gemm(ctypes.byref(g), epi, stream_ptr(a.device)), "pdm_gemm")
+
+
+def mx_quantize_centred(x, stats):
+    """The group-centred MXFP8 copy a producing epilogue writes (include/pdm.h pdm_gemm_args.mx_center): x [R, K]
+    minus mu_t = stats[r, t, 0] / width_t per 256-column group (fp32, as the kernel divides), quantised with
+    mx_quantize."""
+    R, K = x.shape
+    st = stats.reshape(R, -1, 2)
+    xc = x.float().clone()
+    for t in range((K + 255) // 256):
+        w = min(256, K - 256 * t)
+        xc[:, 256 * t: 256 * t + w] -= (st[:, t, 0] / float(w))[:, None]
+    return mx_quantize(xc)
 
 
 def gemm_conv3x3(x, w, bias=None, epi=EPI_F32, up=0, out=None, out_f32=None, accumulate=False):

@@ -80,25 +80,29 @@ struct pdm_uvit {
   // norm1 / norm2 are folded into the next Linear (fused LayerNorm, see GemmArgs): the registered
   // attn.qkv.weight / mlp.fc1.weight are W * diag(norm.weight) in bf16, ln_colsum their row sums and ln_bias
   // W norm.bias (+ the Linear's own bias), both fp32 (include/pdm.h)
-  // a block Linear's weight [N][K]: bf16, or (cfg.fp8) e4m3 bytes + "<key>_scale" E8M0 dwords [K/128][N]
-  void add_lin(const std::string& key, long long N, long long K) {
-    if (cfg.fp8) {
+  // block Linear `bit` (0 qkv, 1 proj, 2 fc1, 3 fc2) runs in MXFP8 (cfg.fp8 / cfg.fp8_linears)
+  bool f8(int bit) const { return cfg.fp8 && (((cfg.fp8_linears ? cfg.fp8_linears : 0xF) >> bit) & 1); }
+  // a block Linear's weight [N][K]: bf16, or (MXFP8) e4m3 bytes + "<key>_scale" E8M0 dwords [K/128][N]; an MXFP8
+  // LayerNorm consumer (qkv, fc1) also takes the bf16 hi / lo group sums "<lin>.ln_gcol" [N][16]
+  void add_lin(const std::string& key, long long N, long long K, int bit, bool ln) {
+    if (f8(bit)) {
       add(key, PDM_FP8, N * K);
       add(key + "_scale", PDM_E8M0, K / 128 * N);
+      if (ln) add(key.substr(0, key.size() - 7) + ".ln_gcol", PDM_BF16, N * 16);
     } else {
       add(key, PDM_BF16, N * K);
     }
   }
   void add_block(const std::string& pre, bool skip) {
-    add_lin(pre + ".attn.qkv.weight", 3LL * D, D);
+    add_lin(pre + ".attn.qkv.weight", 3LL * D, D, 0, true);
     add(pre + ".attn.qkv.ln_colsum", PDM_F32, 3LL * D);
     add(pre + ".attn.qkv.ln_bias", PDM_F32, 3LL * D);
-    add_lin(pre + ".attn.proj.weight", D, D);
+    add_lin(pre + ".attn.proj.weight", D, D, 1, false);
     add(pre + ".attn.proj.bias", PDM_F32, D);
-    add_lin(pre + ".mlp.fc1.weight", Hid, D);
+    add_lin(pre + ".mlp.fc1.weight", Hid, D, 2, true);
     add(pre + ".mlp.fc1.ln_colsum", PDM_F32, Hid);
     add(pre + ".mlp.fc1.ln_bias", PDM_F32, Hid);
-    add_lin(pre + ".mlp.fc2.weight", D, Hid);
+    add_lin(pre + ".mlp.fc2.weight", D, Hid, 3, false);
     add(pre + ".mlp.fc2.bias", PDM_F32, D);
     if (skip) {
       add(pre + ".skip_linear.weight", PDM_BF16, 2LL * D * D);   // bf16 in both modes (run_block8)
@@ -165,7 +169,7 @@ Workspace layout(const pdm_uvit* h, int rows, char* base) {
   const bool f8 = h->cfg.fp8 != 0;   // MXFP8 operands replace XT / MLP; XB / SK stay (bf16 skip_linear)
   w.X = (float*)take(Mx * D * 4);
   w.XB = (bf16*)take(Mx * D * 2);
-  if (!f8) w.XT = (bf16*)take(Mmax * D * 2);
+  if (!f8 || !h->f8(2)) w.XT = (bf16*)take(Mmax * D * 2);   // (fp8 with a bf16 fc1: its A operand)
   w.ST = (float*)take(Mmax * T * 8);
   w.STT = (float*)take(Mmax * T * 8);
   w.QKV = (bf16*)take(Mmax * 3 * D * 2);
@@ -183,7 +187,7 @@ Workspace layout(const pdm_uvit* h, int rows, char* base) {
       return r;
     };
     w.xq = q8(D);
-    w.xtq = q8(D);
+    w.xtq = q8(D);   // skip_linear output (qkv operand), and proj output (fc1 operand) when fc1 is MXFP8
     w.atq = q8(D);
     w.mlq = q8(h->Hid);
   }
@@ -251,6 +255,8 @@ int gemm(const Ctx& c, const bf16* A, int lda, const bf16* W, const float* bias,
 
 // MXFP8 block Linear (cfg.fp8): A and the weight `wkey` (+ "<wkey>_scale") on the block-scaled MFMA; the
 // epilogue also writes the MXFP8 copy of what it stores into `out` when out.q is set (the next Linear's operand)
+// LayerNorm consumers (ln.st_in) take their A operand group-centred (GemmArgs::ln_gcol, "<lin>.ln_gcol"); an
+// MXFP8 output written beside LayerNorm partials (ln.st_out) is group-centred (GemmArgs::mx_center).
 int gemm8(const Ctx& c, const Q8& A, const std::string& wkey, const float* bias, int M, int N, int K, int epi,
           bf16* ob, float* of, int accumulate, LnIO ln, const Q8& out) {
   const pdm_uvit* h = c.h;
@@ -258,6 +264,8 @@ int gemm8(const Ctx& c, const Q8& A, const std::string& wkey, const float* bias,
   const int T = (h->D + 255) / 256;
   a.stats_out = ln.st_out; a.stats_ld = T;
   a.ln_stats = ln.st_in; a.ln_ld = T; a.ln_D = K; a.ln_eps = 1e-5f; a.ln_colsum = ln.colsum;
+  if (ln.st_in) a.ln_gcol = h->w(wkey.substr(0, wkey.size() - 7) + ".ln_gcol");
+  a.mx_center = out.q && ln.st_out ? 1 : 0;
   a.A1 = (const bf16*)A.q; a.lda1 = A.ld; a.K1 = K;
   a.W = (const bf16*)h->ptr(wkey); a.bias = bias;
   a.M = M; a.N = N; a.K = K;
@@ -383,6 +391,7 @@ int run_block8(const Ctx& c, const std::string& pre, float* X, int M, int L, con
     g.out_f32 = X; g.ldr = D;
     g.stats_out = w.STT; g.stats_ld = (D + 255) / 256;
     g.out_fp8 = w.xtq.q; g.ldo8 = w.xtq.ld; g.out_scale = w.xtq.s; g.out_scale_ld = w.xtq.sld;
+    g.mx_center = 1;
     PDM_TRY(launch_gemm(c, g, pdm::EPI_F32));
     a = w.xtq;
     st = w.STT;
@@ -404,18 +413,30 @@ int run_block8(const Ctx& c, const std::string& pre, float* X, int M, int L, con
     PDM_HIP(pdm::attention_launch(at, c.s));
     PDM_HIP(pdm::mxq_launch(w.ATT, 1, D, M, D, w.atq.q, w.atq.ld, w.atq.s, w.atq.sld, c.s));
   }
-  {  // x += proj(attn)
+  const bool fc1_8 = h->f8(2);
+  {  // x += proj(attn) -> X, its partials and the fc1 operand (centred MXFP8, or bf16 for a bf16 fc1)
     LnIO io;
     io.st_out = w.STT;
-    PDM_TRY(gemm8(c, w.atq, pre + ".attn.proj.weight", h->f(pre + ".attn.proj.bias"), M, D, D, pdm::EPI_F32, nullptr,
-                  X, 1, io, w.xtq));
+    PDM_TRY(gemm8(c, w.atq, pre + ".attn.proj.weight", h->f(pre + ".attn.proj.bias"), M, D, D, pdm::EPI_F32,
+                  fc1_8 ? nullptr : w.XT, X, 1, io, fc1_8 ? w.xtq : Q8()));
   }
   {  // h = GELU(fc1(norm2(x))), stored only as the MXFP8 fc2 operand
     LnIO io;
     io.st_in = w.STT;
     io.colsum = h->f(pre + ".mlp.fc1.ln_colsum");
-    PDM_TRY(gemm8(c, w.xtq, pre + ".mlp.fc1.weight", h->f(pre + ".mlp.fc1.ln_bias"), M, h->Hid, D, pdm::EPI_GELU,
-                  nullptr, nullptr, 0, io, w.mlq));
+    if (fc1_8) {
+      PDM_TRY(gemm8(c, w.xtq, pre + ".mlp.fc1.weight", h->f(pre + ".mlp.fc1.ln_bias"), M, h->Hid, D, pdm::EPI_GELU,
+                    nullptr, nullptr, 0, io, w.mlq));
+    } else {   // bf16 MFMA, fused LayerNorm on the bf16 copy, GELU epilogue emitting the MXFP8 fc2 operand only
+      pdm::GemmArgs g{};
+      const int T = (D + 255) / 256;
+      g.A1 = w.XT; g.lda1 = D; g.K1 = D;
+      g.W = h->w(pre + ".mlp.fc1.weight"); g.bias = h->f(pre + ".mlp.fc1.ln_bias");
+      g.M = M; g.N = h->Hid; g.K = D;
+      g.ln_stats = w.STT; g.ln_ld = T; g.ln_D = D; g.ln_eps = 1e-5f; g.ln_colsum = io.colsum;
+      g.out_fp8 = w.mlq.q; g.ldo8 = w.mlq.ld; g.out_scale = w.mlq.s; g.out_scale_ld = w.mlq.sld;
+      PDM_TRY(launch_gemm(c, g, pdm::EPI_GELU));
+    }
   }
   {  // x += fc2(h)
     LnIO io;
@@ -436,7 +457,7 @@ int run_stack8(const Ctx& c, const Workspace& w, int rows, int L) {
   const bool skip = h->cfg.skip != 0;
   const size_t MD = (size_t)M * D;
   PDM_HIP(pdm::rowstats_launch(w.X, D, M, D, nullptr, 0, w.ST, (D + 255) / 256, c.s, w.xq.q, w.xq.ld, w.xq.s,
-                               w.xq.sld));
+                               w.xq.sld, 1));
   for (int i = 0; i < n; ++i)
     PDM_TRY(run_block8(c, "in_blocks." + std::to_string(i), w.X, M, L, w.xq, w.ST, nullptr, nullptr, w.xq,
                        skip ? w.SK + i * MD : nullptr, w.ST, w));
@@ -541,6 +562,9 @@ int pdm_uvit_create(const pdm_uvit_cfg* cfg, pdm_uvit** out) {
   if (c.fp8 && c.t2i) return fail(PDM_ERR_ARG, "fp8: only the class-conditional / unconditional U-ViT has an MXFP8 path");
   if (c.fp8 && (c.embed_dim % 128 || c.mlp_hidden % 128))
     return fail(PDM_ERR_ARG, "fp8: embed_dim and the mlp hidden size must be multiples of 128 (MXFP8 K-tiles)");
+  if (c.fp8 && c.fp8_linears != 0 && c.fp8_linears != 0xF && c.fp8_linears != 0xB)
+    return fail(PDM_ERR_ARG, "fp8_linears: supported sets are all four block Linears (0 / 0xF) and 0xB (mlp.fc1 bf16)");
+  if (c.embed_dim > 2048 && c.fp8) return fail(PDM_ERR_ARG, "fp8: embed_dim must be <= 2048 (centred LayerNorm groups)");
   pdm_uvit* h = new pdm_uvit();
   h->cfg = c;
   h->D = c.embed_dim;
@@ -892,6 +916,7 @@ int pdm_gemm(const pdm_gemm_args* g, int epi, void* stream) {
   a.w_scale = g->w_scale; a.w_scale_ld = g->w_scale_ld;
   a.out_fp8 = (unsigned char*)g->out_fp8; a.ldo8 = g->ldo8;
   a.out_scale = g->out_scale; a.out_scale_ld = g->out_scale_ld;
+  a.mx_center = g->mx_center; a.ln_gcol = (const bf16*)g->ln_gcol;
   PDM_CHECK(pdm::gemm_check(a, epi));
   PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
   return PDM_OK;

@@ -214,6 +214,27 @@ __device__ __forceinline__ void frag_pos(int f, int lane, int wm, int wn, int& m
   }
 }
 
+// (mean, rstd) of a row from its <= 8 LayerNorm partials (sum, M2 per 256-column group; Chan's merge, the
+// arithmetic of ln_merge in the same order) and, when mu != nullptr, every group's mean mu[t] = sum_t / width_t
+// (the centre the producing epilogue subtracted: GemmArgs::mx_center)
+__device__ __forceinline__ float2 ln_from_partials(const float2 (&lst)[8], int ld, int D, float eps, float* mu) {
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) if (t < ld) sum += lst[t].x;
+  const float mean = sum / (float)D;
+  float m2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const float n = (float)min(256, D - 256 * t);
+    if (mu) mu[t] = t < ld ? lst[t].x / n : 0.f;
+    if (t < ld) {
+      const float d = lst[t].x / n - mean;
+      m2 += lst[t].y + n * d * d;
+    }
+  }
+  return make_float2(mean, 1.0f / sqrtf(m2 / (float)D + eps));
+}
+
 // Epilogue of a 256x256 tile (needs 128 KiB of LDS; the staging ring is free by then).
 //  bf16 / GELU: the bf16 tile is written to LDS with a row-XOR chunk swizzle, then stored row-contiguously
 //    with 16-byte stores (full lines, half the store instructions of the per-lane 8-byte scatter).
@@ -222,14 +243,14 @@ __device__ __forceinline__ void frag_pos(int f, int lane, int wm, int wn, int& m
 template <int EPI, int MAP>
 __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc)[32], char* smem, int m0, int n0,
                                             int tid, int lane, int wm, int wn, bool ln_ready = false,
-                                            bool cols_ready = false) {
+                                            bool cols_ready = false, int col_off = COL_LDS) {
   // bias of the lane's 4 column groups, loaded up front with one wave-uniform branch (columns past N read a
   // clamped address and are never stored)
   f32x4 bv[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) bv[g] = f32x4{0.f, 0.f, 0.f, 0.f};
   // cols_ready: the kernel staged the tile's bias / colsum (zeros past N or when absent) at COL_LDS in its prologue
-  const float* lcol = reinterpret_cast<const float*>(smem + COL_LDS);
+  const float* lcol = reinterpret_cast<const float*>(smem + col_off);
   if (EPI != EPI_F32 && cols_ready) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -337,7 +358,7 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
   // threads of a half-wave hold one whole 256-column row, so the LayerNorm partials of the row are two
   // half-wave reductions (sum, then M2 about the group mean)
   const int ncols = min(256, p.N - n0);
-  auto row_stats = [&](const f32x4& a, const f32x4& b, int m, int n) {
+  auto row_stats = [&](const f32x4& a, const f32x4& b, int m, int n) -> float {   // returns the group mean
     float sv = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -358,9 +379,11 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
     for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
     if ((tid & 31) == 0 && m < p.M)
       *reinterpret_cast<float2*>(p.stats_out + ((size_t)m * p.stats_ld + (n0 >> 8)) * 2) = make_float2(sv, q);
+    return mu;
   };
-  auto mx_row = [&](const f32x4& a, const f32x4& b, int m, int n) {   // MXFP8 copy of the stored fp32 row piece
-    const float f[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  // MXFP8 copy of the stored fp32 row piece, minus its 256-column group mean c (mx_center; 0 otherwise)
+  auto mx_row = [&](const f32x4& a, const f32x4& b, int m, int n, float c) {
+    const float f[8] = {a[0] - c, a[1] - c, a[2] - c, a[3] - c, b[0] - c, b[1] - c, b[2] - c, b[3] - c};
     unsigned e8;
     const uint2 q = mx_quant8(f, &e8);
     if (m < p.M && n < p.N) mx_store8(p.out_fp8, p.ldo8, p.out_scale, p.out_scale_ld, m, n, q, e8, (tid & 3) == 0);
@@ -423,18 +446,19 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
             *reinterpret_cast<bf16x8*>(p.out_bf16 + m * p.ldo + n) = o;
           }
         }
+        float mu[4] = {0.f, 0.f, 0.f, 0.f};
         if (p.stats_out) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int idx = (g * 4 + i) * 512 + tid;
-            row_stats(v0[i], v1[i], m0 + pass * 128 + (idx >> 5), n0 + (idx & 31) * 8);
+            mu[i] = row_stats(v0[i], v1[i], m0 + pass * 128 + (idx >> 5), n0 + (idx & 31) * 8);
           }
         }
         if (p.out_fp8) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int idx = (g * 4 + i) * 512 + tid;
-            mx_row(v0[i], v1[i], m0 + pass * 128 + (idx >> 5), n0 + (idx & 31) * 8);
+            mx_row(v0[i], v1[i], m0 + pass * 128 + (idx >> 5), n0 + (idx & 31) * 8, p.mx_center ? mu[i] : 0.f);
           }
         }
       } else {
@@ -460,8 +484,8 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
             v0[i] = a;
             v1[i] = b;
           }
-          if (p.stats_out) row_stats(v0[i], v1[i], m, n);
-          if (p.out_fp8) mx_row(v0[i], v1[i], m, n);
+          const float mu = p.stats_out ? row_stats(v0[i], v1[i], m, n) : 0.f;
+          if (p.out_fp8) mx_row(v0[i], v1[i], m, n, p.mx_center ? mu : 0.f);
         }
       }
     }
@@ -904,28 +928,15 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
   if (tid >= 256) {
     const int n = n0 + tid - 256;
     if (p.bias && n < p.N) cb = p.bias[n];
-    if (ln_pre && n < p.N) cc = p.ln_colsum[n];
+    if (EPI != EPI_F32 && p.ln_stats && n < p.N) cc = p.ln_colsum[n];   // staged even when ln_D > 2048
   }
   auto ln_prologue = [&]() {
     if (tid >= 256) {
       reinterpret_cast<float*>(smem + COL_LDS)[tid - 256] = cb;
       reinterpret_cast<float*>(smem + COL_LDS)[tid] = cc;   // colsum at +256
     }
-    if (ln_pre && tid < 256) {   // ln_merge's arithmetic, in the same order, on the registers
-      float sum = 0.f;
-#pragma unroll
-      for (int t = 0; t < 8; ++t) if (t < p.ln_ld) sum += lst[t].x;
-      const float mean = sum / (float)p.ln_D;
-      float m2 = 0.f;
-#pragma unroll
-      for (int t = 0; t < 8; ++t)
-        if (t < p.ln_ld) {
-          const float n = (float)min(256, p.ln_D - 256 * t);
-          const float d = lst[t].x / n - mean;
-          m2 += lst[t].y + n * d * d;
-        }
-      reinterpret_cast<float2*>(smem + EPI_LDS)[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (float)p.ln_D + p.ln_eps));
-    }
+    if (ln_pre && tid < 256)
+      reinterpret_cast<float2*>(smem + EPI_LDS)[tid] = ln_from_partials(lst, p.ln_ld, p.ln_D, p.ln_eps, nullptr);
   };
 
   f32x4 acc[32];
@@ -1103,7 +1114,10 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 constexpr int MX_SCALE_LDS = EPI_LDS + EPI_LDS_EXTRA;   // 2 x 2 KiB of staged block scales
-constexpr int MX_SMEM = MX_SCALE_LDS + 2 * 2048;
+constexpr int MX_COL_LDS = MX_SCALE_LDS + 2 * 2048;      // the tile's bias [256] + LN colsum [256] (fp32)
+constexpr int MX_ROWC_LDS = MX_COL_LDS + COL_LDS_BYTES;  // centred LN: per row (mu_t - mean) as bf16 hi[8] lo[8]
+constexpr int MX_GCOL_LDS = MX_ROWC_LDS + 256 * 32;      // centred LN: per column c_t as bf16 hi[8] lo[8]
+constexpr int MX_SMEM = MX_GCOL_LDS + 256 * 32;          // 152 KiB
 
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_mx_kernel(GemmArgs p, int tiles_n, int nwg) {
@@ -1240,6 +1254,32 @@ __global__ __launch_bounds__(512, 1) void gemm_mx_kernel(GemmArgs p, int tiles_n
     __builtin_amdgcn_s_setprio(0);
   };
 
+  // epilogue inputs fetched ahead of the first operand DMA (as gemm8d_kernel): the tile's LayerNorm row partials
+  // (waves 0-3, one row each), its bias / LN column sums or, for the centred LayerNorm (GemmArgs::ln_gcol), the
+  // bf16 hi / lo group sums of its columns (waves 4-7, one column each); the prologue's vmcnt wait covers them
+  const bool ln_pre = EPI != EPI_F32 && p.ln_stats != nullptr && p.ln_ld <= 8;
+  const bool lnc = ln_pre && p.ln_gcol != nullptr;
+  float2 lst[8];
+  if (ln_pre && tid < 256) {
+    const float2* st = reinterpret_cast<const float2*>(p.ln_stats) + (size_t)min(m0 + tid, p.M - 1) * p.ln_ld;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) lst[t] = t < p.ln_ld ? st[t] : make_float2(0.f, 0.f);
+  }
+  float cb = 0.f, cc = 0.f;
+  i32x4 gc[2] = {i32x4{0, 0, 0, 0}, i32x4{0, 0, 0, 0}};
+  if (tid >= 256) {
+    const int n = n0 + tid - 256;
+    if (n < p.N) {
+      if (p.bias) cb = p.bias[n];
+      if (EPI != EPI_F32 && p.ln_stats && !lnc) cc = p.ln_colsum[n];
+      if (lnc) {
+        const i32x4* src = reinterpret_cast<const i32x4*>(p.ln_gcol + (size_t)n * 16);
+        gc[0] = src[0];
+        gc[1] = src[1];
+      }
+    }
+  }
+
   issue_scales(0);
   issue(0, KA0);
   issue(0, KW0);
@@ -1253,6 +1293,34 @@ __global__ __launch_bounds__(512, 1) void gemm_mx_kernel(GemmArgs p, int tiles_n
     asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  }
+  if (tid >= 256) {
+    reinterpret_cast<float*>(smem + MX_COL_LDS)[tid - 256] = cb;
+    reinterpret_cast<float*>(smem + MX_COL_LDS)[tid] = cc;   // colsum at +256 (zero for the centred form)
+    if (lnc) {
+      i32x4* dst = reinterpret_cast<i32x4*>(smem + MX_GCOL_LDS + (tid - 256) * 32);
+      dst[0] = gc[0];
+      dst[1] = gc[1];
+    }
+  }
+  if (ln_pre && tid < 256) {
+    float mu[8];
+    const float2 mr = ln_from_partials(lst, p.ln_ld, p.ln_D, p.ln_eps, lnc ? mu : nullptr);
+    if (lnc) {   // rows carry (mu_t - mean) as a bf16 pair; the epilogue then sees mean 0
+      bf16x8 hi, lo;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const float d = mu[t] - mr.x;
+        hi[t] = (bf16)d;
+        lo[t] = (bf16)(d - (float)hi[t]);
+      }
+      bf16x8* dst = reinterpret_cast<bf16x8*>(smem + MX_ROWC_LDS + tid * 32);
+      dst[0] = hi;
+      dst[1] = lo;
+      reinterpret_cast<float2*>(smem + EPI_LDS)[tid] = make_float2(0.f, mr.y);
+    } else {
+      reinterpret_cast<float2*>(smem + EPI_LDS)[tid] = mr;
+    }
   }
   bar_raw();
   if (wave >= 4) bar_raw();
@@ -1288,7 +1356,41 @@ __global__ __launch_bounds__(512, 1) void gemm_mx_kernel(GemmArgs p, int tiles_n
     bar_raw();
   }
   if (wave < 4) bar_raw();
-  epilogue256<EPI, 1>(p, acc, smem, m0, n0, tid, lane, wm, wn);
+  if (lnc) {
+    // centred LayerNorm: acc += sum_t (mu_t - mean) c_t as one bf16 MFMA per accumulator; K lanes 0-7 carry
+    // hi * hi, 8-15 hi * lo, 16-23 lo * hi, 24-31 zeros (tables written before the prologue barrier)
+    const int kg = lane >> 4;
+    const bf16x8 z8 = __builtin_bit_cast(bf16x8, i32x4{0, 0, 0, 0});
+    bf16x8 wc[2][2];
+#pragma unroll
+    for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int col = qj * 128 + wn * 32 + ni * 16 + (lane & 15);
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + MX_GCOL_LDS + col * 32 + (kg == 1 ? 16 : 0));
+        wc[qj][ni] = kg == 3 ? z8 : v;
+      }
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+      bf16x8 ac[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int row = qi * 128 + wm * 64 + mi * 16 + (lane & 15);
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + MX_ROWC_LDS + row * 32 + (kg == 2 ? 16 : 0));
+        ac[mi] = kg == 3 ? z8 : v;
+      }
+#pragma unroll
+      for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) {
+            f32x4& c = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
+            c = mfma16x16x32(wc[qj][ni], ac[mi], c);
+          }
+    }
+  }
+  epilogue256<EPI, 1>(p, acc, smem, m0, n0, tid, lane, wm, wn, ln_pre, true, MX_COL_LDS);
 }
 }  // namespace
 
@@ -1322,6 +1424,10 @@ const char* gemm_check(const GemmArgs& p, int epi) {
     if (!p.a_scale || !p.w_scale || p.a_scale_ld < p.M || p.w_scale_ld < p.N || (p.lda1 % 16) || (p.ldw && p.ldw % 16))
       return "gemm(fp8): block scales missing or leading dimensions not multiples of 16 bytes";
   }
+  if (p.mx_center && (!p.out_fp8 || !p.stats_out || epi != EPI_F32))
+    return "gemm: mx_center needs the fp32 epilogue with both stats_out and the MXFP8 output";
+  if (p.ln_gcol && (!p.fp8 || !p.ln_stats || p.ln_ld > 8 || ((uintptr_t)p.ln_gcol & 15)))
+    return "gemm: ln_gcol (centred LayerNorm) needs an MXFP8 A operand, ln_stats with ln_D <= 2048 and 16-byte alignment";
   if (p.ln_stats) {
     if (epi == EPI_F32) return "gemm: the fused LayerNorm applies to the bf16 / GELU epilogues";
     if (!p.ln_colsum || ((uintptr_t)p.ln_colsum & 15) || p.ln_D <= 0 || p.ln_ld != (p.ln_D + 255) / 256)

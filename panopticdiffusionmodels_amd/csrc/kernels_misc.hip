@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs p) {
 template <int NV>
 __global__ __launch_bounds__(256) void rowstats_kernel(const float* x, int ldx, int rows, int D, bf16* xb, int ldb,
                                                        float* stats, int stats_ld, unsigned char* xq, int ldq,
-                                                       unsigned* xs, int xs_ld) {
+                                                       unsigned* xs, int xs_ld, int center) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + wave;
   if (r >= rows) return;
@@ -79,18 +79,18 @@ __global__ __launch_bounds__(256) void rowstats_kernel(const float* x, int ldx, 
     const bool ok = idx < nv;
     const f32x4 v = ok ? xr[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
     if (ok && xb) *reinterpret_cast<bf16x4*>(xb + (size_t)r * ldb + 4 * idx) = to_bf16x4(v[0], v[1], v[2], v[3]);
-    if (xq) {   // MXFP8 copy: 8 consecutive lanes hold one 32-column block
+    const float s = wave_sum((v[0] + v[1]) + (v[2] + v[3]));
+    const float mu = s / (float)min(256, D - 256 * i);
+    const f32x4 d = v - mu;
+    if (xq) {   // MXFP8 copy (group-centred: GemmArgs::mx_center): 8 consecutive lanes hold one 32-column block
       unsigned e8;
-      const unsigned q = mx_quant4(v, &e8);
+      const unsigned q = mx_quant4(center ? d : v, &e8);
       if (ok) {
         *reinterpret_cast<unsigned*>(xq + (size_t)r * ldq + 4 * idx) = q;
         if ((lane & 7) == 0)
           reinterpret_cast<unsigned char*>(xs)[((size_t)(idx >> 5) * xs_ld + r) * 4 + ((idx >> 3) & 3)] = (unsigned char)e8;
       }
     }
-    const float s = wave_sum((v[0] + v[1]) + (v[2] + v[3]));
-    const float mu = s / (float)min(256, D - 256 * i);
-    const f32x4 d = v - mu;
     const float q = wave_sum(ok ? (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]) : 0.f);
     if (lane == 0) *reinterpret_cast<float2*>(stats + ((size_t)r * stats_ld + i) * 2) = make_float2(s, q);
   }
@@ -413,13 +413,13 @@ hipError_t layernorm_launch(const LayerNormArgs& p, hipStream_t stream) {
 }
 
 hipError_t rowstats_launch(const float* x, int ldx, int rows, int D, bf16* xb, int ldb, float* stats, int stats_ld,
-                           hipStream_t stream, unsigned char* xq, int ldq, unsigned* xs, int xs_ld) {
+                           hipStream_t stream, unsigned char* xq, int ldq, unsigned* xs, int xs_ld, int center) {
   if (!x || !stats || rows <= 0 || D <= 0 || D % 4 || D > 2048 || stats_ld < (D + 255) / 256 || ldx % 4 ||
       (xb && ldb % 4) || (xq && (D % 32 || ldq % 4 || !xs || xs_ld < rows)))
     return hipErrorInvalidValue;
   dim3 grid((rows + 3) / 4), block(256);
   hipLaunchKernelGGL(rowstats_kernel<8>, grid, block, 0, stream, x, ldx, rows, D, xb, ldb, stats, stats_ld, xq, ldq,
-                     xs, xs_ld);
+                     xs, xs_ld, center);
   return hipGetLastError();
 }
 

@@ -51,6 +51,19 @@ struct GemmArgs {
   // 2^ceil(log2(amax/448)) per 32 columns, so no element saturates)
   unsigned char* out_fp8; int ldo8;
   unsigned* out_scale; int out_scale_ld;
+  // Group-centred MXFP8 LayerNorm operands (the fp8 forward's norm1 -> qkv / norm2 -> fc1).  e4m3 keeps 3
+  // mantissa bits of every element, so quantising the RAW residual row x loses the LayerNorm's signal
+  // x - mean once |mean| >> std.  Instead:
+  //  producer (EPI_F32 with stats_out, out_fp8 and mx_center): the MXFP8 copy holds x - mu_t, mu_t = the mean of
+  //    the row's 256-column group t, i.e. exactly stats_out's sum / group width
+  //  consumer (fp8, EPI_BF16 / EPI_GELU with ln_stats and ln_gcol): A = MX(x - mu_t); ln_gcol [N][16] bf16 holds
+  //    per output column n the group sums c_t[n] = sum_{k in group t} W[n][k] of the dequantised weight as a
+  //    bf16 pair (hi [0..7], lo [8..15], t < 8, zero padded), and
+  //      out[m, n] = rstd_m * (acc + sum_t (mu_t - mean_m) * c_t[n]) + bias[n]
+  //    where the rank-ceil(K/256) correction runs as one extra bf16 MFMA per accumulator with the split
+  //    products hi*hi + hi*lo + lo*hi (fp32-level accuracy) and ln_colsum is unused
+  int mx_center;
+  const bf16* ln_gcol;
   // tuning knobs (set by gemm_launch): raster = row panels per tile group inside an XCD's range (0: row-major);
   // dbg_tile0 = stage every tile's operands from tile (0, 0) (timing experiments only: wrong results)
   int raster, dbg_tile0;
@@ -63,9 +76,10 @@ void gemm_set_tuning(int raster, int dbg_tile0);
 // Row partials of the fused LayerNorm: X fp32 [rows, D] -> stats [rows, ceil(D/256)] (sum, M2) per 256-column
 // group (+ optional bf16 copy xb [rows, D], + optional MXFP8 copy xq / xs in the GemmArgs A-operand layout).  Used where no GEMM epilogue produced them (token assembly, the
 // t2i mask-stream refresh, and behind the 128-tile GEMM policy).
+// The MXFP8 copy is group-centred (x - mu_t, GemmArgs::mx_center) when center != 0.
 hipError_t rowstats_launch(const float* x, int ldx, int rows, int D, bf16* xb, int ldb, float* stats, int stats_ld,
                            hipStream_t stream, unsigned char* xq = nullptr, int ldq = 0, unsigned* xs = nullptr,
-                           int xs_ld = 0);
+                           int xs_ld = 0, int center = 0);
 
 const char* gemm_check(const GemmArgs& p, int epi);
 hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream);

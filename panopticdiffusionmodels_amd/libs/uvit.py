@@ -110,14 +110,23 @@ class UViT(HipNet):
         return dict(img_size=self.img_size, patch_size=self.patch_size, in_chans=self.in_chans,
                     embed_dim=self.embed_dim, depth=self.depth, num_heads=self.num_heads, mlp_ratio=self.mlp_ratio,
                     num_classes=self.num_classes, conv=self.conv, skip=self.skip, qkv_bias=self.qkv_bias,
-                    mlp_time_embed=self.mlp_time_embed, fp8=self.precision == "fp8")
+                    mlp_time_embed=self.mlp_time_embed, fp8=self.precision != "bf16",
+                    fp8_linears=self.FP8_LINEARS[self.precision])
+
+    # include/pdm.h pdm_uvit_cfg.fp8_linears: bit 0 attn.qkv, 1 attn.proj, 2 mlp.fc1, 3 mlp.fc2
+    FP8_LINEARS = {"bf16": 0, "fp8": 0xB, "fp8-all": 0xF}
 
     def set_precision(self, precision):
-        """'bf16' (default) or 'fp8': the block Linears (qkv, proj, fc1, fc2, skip_linear) as MXFP8 GEMMs on the
-        block-scaled MFMA, every other op unchanged (BASELINE configs[4], imagenet512_uvit_huge; include/pdm.h
-        pdm_uvit_cfg.fp8).  Not a reference option: the reference computes in the autocast dtype."""
-        if precision not in ("bf16", "fp8"):
-            raise ValueError(f"precision must be 'bf16' or 'fp8', got {precision!r}")
+        """Precision of the block Linears (BASELINE configs[4], imagenet512_uvit_huge; include/pdm.h
+        pdm_uvit_cfg.fp8 / fp8_linears).  Not a reference option: the reference computes in the autocast dtype.
+          'bf16'    (default) every GEMM bf16
+          'fp8'     attn.qkv, attn.proj, mlp.fc2 as MXFP8 GEMMs on the block-scaled MFMA, mlp.fc1 and
+                    skip_linear bf16: H/4 forward 5.0e-2 rel-L2 vs fp32 (within SURVEY.md §8c's 6e-2)
+          'fp8-all' mlp.fc1 MXFP8 too (6.9e-2; tools/fp8_ablation.py prints the per-Linear ablation)
+        Everything else (attention, norms, heads) is unchanged.  Re-packs the weights (invalidates the handle; a
+        sampler's captured graph is recaptured on the next sample)."""
+        if precision not in self.FP8_LINEARS:
+            raise ValueError(f"precision must be one of {sorted(self.FP8_LINEARS)}, got {precision!r}")
         self.precision = precision
         self.invalidate()
         return self

@@ -37,7 +37,23 @@ def cfg_struct(kw, t2i):
     c.enable_panoptic = int(bool(kw.get("enable_panoptic", True))) if t2i else 0
     c.num_panoptic_class = int(kw.get("num_panoptic_class", 8)) if t2i else 0
     c.fp8 = int(bool(kw.get("fp8", False)))
+    c.fp8_linears = int(kw.get("fp8_linears", 0)) if c.fp8 else 0
     return c
+
+
+def gcol_table(w):
+    """[N, K] (dequantised) weight -> bf16 [N, 16]: per row n the sums c_t of its 256-column groups t < 8 as a
+    bf16 pair, hi at [t], lo = bf16(c_t - hi) at [8 + t] (include/pdm.h pdm_gemm_args.ln_gcol)."""
+    N, K = w.shape
+    G = (K + 255) // 256
+    if G > 8:
+        raise ValueError(f"centred LayerNorm supports K <= 2048, got {K}")
+    c = torch.zeros(N, 8, dtype=torch.float64, device=w.device)
+    for t in range(G):
+        c[:, t] = w[:, 256 * t: 256 * (t + 1)].double().sum(1)
+    hi = c.float().bfloat16()
+    lo = (c.float() - hi.float()).bfloat16()
+    return torch.cat([hi, lo], 1).contiguous()
 
 
 class NativeHandle:
@@ -57,14 +73,16 @@ class NativeHandle:
         dev = next(iter(sd.values())).device
         n = lib.pdm_uvit_param_count(h)
         buf = ctypes.create_string_buffer(256)
+        self.dtypes = {}
         for i in range(n):
             dt = ctypes.c_int()
             numel = ctypes.c_longlong()
             _lib.check(lib.pdm_uvit_param_info(h, i, buf, 256, ctypes.byref(dt), ctypes.byref(numel)))
-            name = buf.value.decode()
-            t = self._pack(sd, name, dt.value, numel.value, dev)
+            self.dtypes[buf.value.decode()] = (dt.value, numel.value)
+        for name, (dt, numel) in self.dtypes.items():
+            t = self._pack(sd, name, dt, numel, dev)
             self.packed[name] = t
-            _lib.check(lib.pdm_uvit_set_param(h, name.encode(), ctypes.c_void_p(t.data_ptr()), dt.value, t.numel()),
+            _lib.check(lib.pdm_uvit_set_param(h, name.encode(), ctypes.c_void_p(t.data_ptr()), dt, t.numel()),
                        "pdm_uvit_set_param")
         _lib.check(lib.pdm_uvit_validate(h), "pdm_uvit_validate")
         self._mx = {}
@@ -96,15 +114,17 @@ class NativeHandle:
 
     def _mx_weight(self, sd, key, dev):
         """MXFP8 copy of a block Linear weight [N, K] (norm-folded for attn.qkv / mlp.fc1): e4m3 bytes, E8M0 scale
-        dwords [K/128, N] (the quantiser of the GPU epilogues, _lib.mx_quantize) and the row sums of the
-        DEQUANTISED weight, which the fused LayerNorm subtracts (mean * colsum must cancel exactly what the MFMA
-        multiplies)."""
+        dwords [K/128, N] (the quantiser of the GPU epilogues, _lib.mx_quantize), the row sums of the DEQUANTISED
+        weight (what the fused LayerNorm's mean * colsum must cancel) and their per-256-column-group split as the
+        bf16 hi / lo table [N, 16] of the centred LayerNorm (include/pdm.h pdm_gemm_args.ln_gcol)."""
         if key not in self._mx:
             w = self._ln_fold(sd, key, fp32=True)
             if w is None:
                 w = sd[key].detach().float()
             q, s = _lib.mx_quantize(w.to(dev))
-            self._mx[key] = (q, s, _lib.mx_dequantize(q, s).double().sum(1).float())
+            dq = _lib.mx_dequantize(q, s).double()
+            lnc = key.endswith((".attn.qkv.weight", ".mlp.fc1.weight"))   # the LayerNorm consumers
+            self._mx[key] = (q, s, dq.sum(1).float(), gcol_table(dq) if lnc else None)
         return self._mx[key]
 
     def _pack(self, sd, name, dtype, numel, dev):
@@ -114,7 +134,9 @@ class NativeHandle:
                 t = self._mx_weight(sd, name, dev)[0].view(torch.uint8).reshape(-1)
             elif dtype == _lib.PDM_E8M0:
                 t = self._mx_weight(sd, name[: -len("_scale")], dev)[1].reshape(-1)
-            elif name.endswith(".ln_colsum"):
+            elif name.endswith(".ln_gcol"):
+                t = self._mx_weight(sd, name[: -len(".ln_gcol")] + ".weight", dev)[3].reshape(-1)
+            elif name.endswith(".ln_colsum") and self.dtypes[name[: -len(".ln_colsum")] + ".weight"][0] == _lib.PDM_FP8:
                 t = self._mx_weight(sd, name[: -len(".ln_colsum")] + ".weight", dev)[2]
             if t is not None:
                 if t.numel() != numel:
@@ -171,19 +193,28 @@ class HipNet(nn.Module):
     def __init__(self):
         super().__init__()
         self._native = None
+        self._generation = 0
 
     def _native_cfg_kwargs(self):
         raise NotImplementedError
 
     def invalidate(self):
+        """Drops the packed weights and workspace.  Every (re)build of the handle bumps `generation`, so a
+        holder of device addresses taken from an older handle (a captured HIP graph, sampler.py) can tell
+        that they are stale."""
         self._native = None
 
+    @property
+    def generation(self):
+        """Identifies the current native handle (and so every device address it owns); -1 = none built."""
+        return self._generation if self._native is not None else -1
+
     def _apply(self, fn, *args, **kwargs):
-        self._native = None
+        self.invalidate()
         return super()._apply(fn, *args, **kwargs)
 
     def load_state_dict(self, state_dict, strict=True, *args, **kwargs):
-        self._native = None
+        self.invalidate()
         return super().load_state_dict(state_dict, strict, *args, **kwargs)
 
     def native(self):
@@ -191,4 +222,5 @@ class HipNet(nn.Module):
             p = next(self.parameters())
             _lib.require_gpu(p)
             self._native = NativeHandle(self, cfg_struct(self._native_cfg_kwargs(), self._t2i))
+            self._generation += 1
         return self._native

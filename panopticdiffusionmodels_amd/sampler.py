@@ -40,6 +40,14 @@ def build_plan(front_end, steps=50, eps=None, betas=None):
     raise ValueError(f"unknown solver front-end {front_end!r}")
 
 
+def _drop_stale_graph(st, nnet):
+    """A captured graph holds the device addresses of the net's packed weights and workspace.  Anything that
+    rebuilds the native handle (load_state_dict, .to(), set_precision) frees those, so the graph is dropped and
+    recaptured on the new handle rather than replayed on freed memory."""
+    if st["graph"] is not None and st.get("generation") != nnet.generation:
+        st["graph"] = None
+
+
 class ClassCondSampler:
     """z_T -> z_0 for a class-conditional (or unconditional) UViT with CFG, fully on the GPU.
 
@@ -121,6 +129,7 @@ class ClassCondSampler:
         if not self.use_graph or eager:
             self._loop(st, B)
             return st["x"].clone()
+        _drop_stale_graph(st, self.nnet)
         if st["graph"] is None:
             # warm-up outside capture: builds the native handle, workspace and conv params
             self._loop(st, B)
@@ -132,7 +141,7 @@ class ClassCondSampler:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._loop(st, B)
-            st["graph"] = g
+            st["graph"], st["generation"] = g, self.nnet.generation
         st["graph"].replay()
         return st["x"].clone()
 
@@ -224,6 +233,7 @@ class T2ISampler:
         if not self.use_graph:
             self._loop(st, B)
         else:
+            _drop_stale_graph(st, self.nnet)
             if st["graph"] is None:
                 self._loop(st, B)
                 load()
@@ -231,6 +241,6 @@ class T2ISampler:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self._loop(st, B)
-                st["graph"] = g
+                st["graph"], st["generation"] = g, self.nnet.generation
             st["graph"].replay()
         return st["x"].clone(), st["pm"][0].clone()

@@ -1,7 +1,10 @@
 """Generate tests/golden/fullsize.npz: the REFERENCE's own outputs at every BASELINE config's full size (build
 container only; SURVEY.md §8c "full-size configs").
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_fullsize_golden.py [/root/reference]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_fullsize_golden.py [/root/reference] [--only sample:<config>,...]
+
+`--only` regenerates just the named entries (fwd:<config> / sample:<config>) and merges them into the existing
+fullsize.npz (every entry is deterministic, so the others are unchanged by a full run).
 
 Weights and inputs come from this repo's seeded generators (panopticdiffusionmodels_amd.weights,
 make_golden._inputs), so only outputs and checksums are stored:
@@ -25,7 +28,7 @@ from make_golden import C, W, _import_reference, _inputs, _np, _sd_checksum  # n
 
 CONFIGS = ["cifar10_uvit_small", "imagenet256_uvit_large", "imagenet256_uvit_huge", "imagenet512_uvit_huge",
            "mscoco_uvit_small"]
-SAMPLE_CONFIGS = ["imagenet256_uvit_large", "imagenet256_uvit_huge", "mscoco_uvit_small"]
+SAMPLE_CONFIGS = ["imagenet256_uvit_large", "imagenet256_uvit_huge", "imagenet512_uvit_huge", "mscoco_uvit_small"]
 BETAS = (torch.linspace(0.00085 ** 0.5, 0.0120 ** 0.5, 1000, dtype=torch.float64) ** 2).numpy()
 
 
@@ -55,8 +58,8 @@ def _net(mods, name, seed, init):
     return net.eval(), sd
 
 
-def gen_forward(mods, out):
-    for name in CONFIGS:
+def gen_forward(mods, out, names=CONFIGS):
+    for name in names:
         net, sd = _net(mods, name, 3, "random")
         inp = _inputs(name, 2, seed=5)
         with torch.no_grad():
@@ -71,9 +74,9 @@ def gen_forward(mods, out):
         print("fwd", name, tuple(eps.shape), flush=True)
 
 
-def gen_sample(mods, out):
+def gen_sample(mods, out, names=SAMPLE_CONFIGS):
     _, _, _, pp, dpt, sde = mods
-    for name in SAMPLE_CONFIGS:
+    for name in names:
         full = C.get_config(name)
         net, sd = _net(mods, name, 0, "reference")
         inp = sample_inputs(name)
@@ -125,13 +128,25 @@ def gen_sample(mods, out):
 
 
 def main():
-    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    argv = list(sys.argv[1:])
+    only = None
+    if "--only" in argv:
+        i = argv.index("--only")
+        only = argv[i + 1].split(",")
+        del argv[i:i + 2]
+    ref = argv[0] if argv else "/root/reference"
     mods = _import_reference(ref)
     torch.set_num_threads(8)
-    out = {}
-    gen_forward(mods, out)
-    gen_sample(mods, out)
     path = os.path.join(HERE, "fullsize.npz")
+    if only is None:
+        out = {}
+        gen_forward(mods, out)
+        gen_sample(mods, out)
+    else:
+        with np.load(path) as f:
+            out = {k: f[k] for k in f.files}
+        gen_forward(mods, out, [e.split(":", 1)[1] for e in only if e.startswith("fwd:")])
+        gen_sample(mods, out, [e.split(":", 1)[1] for e in only if e.startswith("sample:")])
     np.savez_compressed(path, **{k: np.asarray(v) for k, v in out.items()})
     print(f"wrote {path}: {len(out)} arrays, {os.path.getsize(path) / 1e6:.2f} MB")
 
