@@ -201,8 +201,7 @@ def main():
         sampler.sample(zs[-1], ys[-1], eager=True)
     prof.disable()
     torch.cuda.synchronize(dev)
-    roof = gemm_roofline(prof, ncfg, 2 * B if t2i or sampler.cfg else B, precision,
-                         with_traffic=args.config == "imagenet256_uvit_large" and B == 95)
+    roof = gemm_roofline(prof, ncfg, 2 * B if t2i or sampler.cfg else B, precision, config=args.config)
     samp_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
 
@@ -257,27 +256,28 @@ def metric_name(config, zshape, with_decode):
             f"{f', {res}x{res} decode' if with_decode else ', latents only (no decode)'}")
 
 
-def measured_traffic():
-    """HBM bytes per GEMM launch from the newest committed PMC summary (tools/profile_bench.sh +
-    tools/summarize_prof.py: FETCH_SIZE x 2 + WRITE_SIZE, separate rocprofv3 passes), or None."""
+def measured_traffic(config, rows, precision):
+    """HBM bytes per GEMM launch from the newest committed PMC summary of this config / batch / precision
+    (tools/profile_bench.sh + tools/summarize_prof.py: FETCH_SIZE x 2 + WRITE_SIZE, separate rocprofv3 passes),
+    or None when no summary was collected for these shapes."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    fam = d.get("gemm_family")
-    return (fam["hbm_bytes_per_launch"] if fam else None), os.path.basename(files[-1])
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), reverse=True):
+        d = json.load(open(f))
+        key = (d.get("config", "imagenet256_uvit_large"), d.get("rows", 190), d.get("precision", "bf16"))
+        if key == (config, rows, precision) and d.get("gemm_family"):
+            return d["gemm_family"]["hbm_bytes_per_launch"], os.path.basename(f)
+    return None, None
 
 
-def gemm_roofline(prof, ncfg, rows, precision="bf16", with_traffic=True):
-    """GEMM-family roofline; `traffic` only for the shapes the committed PMC summary was collected on (the
-    default L/2 bench batch), null otherwise."""
+def gemm_roofline(prof, ncfg, rows, precision="bf16", config="imagenet256_uvit_large"):
+    """GEMM-family roofline; `traffic` from the committed PMC summary of these shapes (config, rows,
+    precision), null when none was collected."""
     times_ms, flops = prof.read()
     n = len(times_ms)
     tot_t = sum(times_ms) / 1e3
     tot_f = sum(flops)
     achieved = tot_f / tot_t
-    traffic, tsrc = measured_traffic() if precision == "bf16" and with_traffic else (None, None)  # noqa
+    traffic, tsrc = measured_traffic(config, rows, precision)
     kernel = "bf16 GEMM family (all U-ViT linear layers: qkv, proj, fc1, fc2, skip_linear" + \
         (", context_embed, zero_convs)" if ncfg["name"] == "uvit_t2i" else ")")
     peak = PEAK_BF16

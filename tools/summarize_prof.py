@@ -1,11 +1,12 @@
-"""Turn a tools/profile_bench.sh run (gpurun_out/prof_TAG) into the committed evidence under profiles/:
+"""Turn a tools/profile_bench.sh run (gpurun_out/prof_TAG_CONFIG) into the committed evidence under profiles/:
 
-  profiles/TAG_bench_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the bench command
-  profiles/TAG_traffic.json             per-kernel HBM traffic per launch from the FETCH_SIZE / WRITE_SIZE
-                                        passes (FETCH_SIZE doubled: MI355X_MICROARCH.md §HBM, 16-B streaming
-                                        reads are tallied at half their bytes; values are KiB in rocprofv3)
+  profiles/TAG_CONFIG_bench_kernel_stats.csv  rocprofv3 --kernel-trace --stats summary of the bench command
+  profiles/TAG_CONFIG_traffic.json            per-kernel HBM traffic per launch from the FETCH_SIZE / WRITE_SIZE
+                                              passes (FETCH_SIZE doubled: MI355X_MICROARCH.md §HBM, 16-B streaming
+                                              reads are tallied at half their bytes; values are KiB in rocprofv3),
+                                              keyed by config / rows / precision for bench.py measured_traffic()
 
-Usage: python tools/summarize_prof.py TAG
+Usage: python tools/summarize_prof.py TAG [CONFIG [BATCH [PRECISION]]]
 """
 import csv
 import json
@@ -35,16 +36,20 @@ def per_kernel(path, counter):
 
 def main():
     tag = sys.argv[1]
-    src = os.path.join(REPO, "gpurun_out", f"prof_{tag}")
+    config = sys.argv[2] if len(sys.argv) > 2 else "imagenet256_uvit_large"
+    batch = int(sys.argv[3]) if len(sys.argv) > 3 else 95
+    precision = sys.argv[4] if len(sys.argv) > 4 else "bf16"
+    src = os.path.join(REPO, "gpurun_out", f"prof_{tag}_{config}")
     dst = os.path.join(REPO, "profiles")
     os.makedirs(dst, exist_ok=True)
     kt = os.path.join(src, "kt", "run_kernel_stats.csv")
     if os.path.exists(kt):
-        shutil.copy(kt, os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))
+        shutil.copy(kt, os.path.join(dst, f"{tag}_{config}_bench_kernel_stats.csv"))
     fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
-    out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over tools/time_forward.py "
-                     f"imagenet256_uvit_large 190 (one CFG forward at the bench batch, 95 images x 2 rows)",
+    out = {"config": config, "rows": 2 * batch, "precision": precision,
+           "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over tools/time_forward.py "
+                     f"{config} {2 * batch} 2 {precision} (CFG forwards at the bench batch, {batch} images x 2 rows)",
            "correction": "fetch_bytes = FETCH_SIZE[KiB] x 1024 x 2 (gfx950 tallies 16-B streaming reads at half); "
                          "write_bytes = WRITE_SIZE[KiB] x 1024",
            "kernels": {}}
@@ -60,7 +65,7 @@ def main():
             gemm_n += n
     if gemm_n:
         out["gemm_family"] = {"launches": int(gemm_n), "hbm_bytes_per_launch": round((gemm_f + gemm_w) / gemm_n)}
-    json.dump(out, open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(dst, f"{tag}_{config}_traffic.json"), "w"), indent=1)
     print(json.dumps(out.get("gemm_family"), indent=1))
 
 

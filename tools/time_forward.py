@@ -17,18 +17,23 @@ cfg = configs.nnet_kwargs(name)
 sd = weights.nnet_state_dict(cfg, seed=0, device=dev)
 net = get_nnet(**cfg).to(dev)
 net.load_state_dict(sd)
-net.set_precision(precision)
+if precision != "bf16":
+    net.set_precision(precision)
 zs = configs.get_config(name)["z_shape"]
 x = torch.randn(rows, *zs, device=dev)
 t = torch.rand(rows, device=dev) * 999
-y = torch.randint(0, 1000, (rows,), device=dev) if cfg.get("num_classes", -1) > 0 else None
+if cfg["name"] == "uvit_t2i":   # context + panoptic mask token (libs/uvit_t2i.py:378)
+    extra = (torch.randn(rows, cfg["num_clip_token"], cfg["clip_dim"], device=dev),
+             torch.randn(rows, cfg["num_panoptic_class"], *zs[1:], device=dev))
+else:
+    extra = (torch.randint(0, 1000, (rows,), device=dev) if cfg.get("num_classes", -1) > 0 else None,)
 with torch.no_grad():
     for _ in range(3):
-        net.forward_pre(x, t, y)
+        net.forward_pre(x, t, *extra)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(n):
-        net.forward_pre(x, t, y)
+        net.forward_pre(x, t, *extra)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / n
 D, depth = cfg["embed_dim"], cfg["depth"]
