@@ -78,6 +78,10 @@ typedef struct pdm_uvit_cfg {
    * Supported: 0 / 0xF, and 0xB (mlp.fc1 in bf16: the forward error of the H/4 net drops from 6.9e-2 to
    * 5.0e-2 rel-L2, tools/fp8_ablation.py).  A bf16 Linear's weight is registered as in the bf16 path. */
   int fp8_linears;
+  /* residual stream precision between blocks.  0 (default): bf16, as the reference's own GPU run keeps it under
+   * autocast (each Linear output is added to x in the autocast dtype); 1: fp32.  The t2i and MXFP8 forwards
+   * always keep it fp32. */
+  int residual_fp32;
 } pdm_uvit_cfg;
 
 /* replaces utils.get_nnet (utils.py:291-299) + UViT.__init__ (libs/uvit.py:139-195) */
@@ -183,6 +187,9 @@ typedef struct pdm_gemm_args {
    *   out = rstd * (A W^T + sum_t (mu_t - mean) c_t) + bias   (ln_colsum then unused) */
   int mx_center;
   const void* ln_gcol;
+  /* epi = 3 (residual on a bf16 stream): out_bf16 = bf16(A W^T + bias (+ res_in when accumulate)), LayerNorm
+   * partials of the rounded values to stats_out; res_in [M][ldri] bf16 may alias out_bf16 */
+  const void* res_in; int ldri;
 } pdm_gemm_args;
 int pdm_gemm(const pdm_gemm_args* a, int epi, void* stream);
 /* Implicit-GEMM conv3x3 (stride 1, pad 1) on NHWC bf16 input [B, H>>up, W>>up, Cin] (up = 1: the nearest-x2

@@ -13,14 +13,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpdm.so")
 
 PDM_F32, PDM_BF16, PDM_FP8, PDM_E8M0 = 0, 1, 2, 3
-EPI_BF16, EPI_GELU, EPI_F32 = 0, 1, 2
+EPI_BF16, EPI_GELU, EPI_F32, EPI_RES = 0, 1, 2, 3
 
 
 class PdmUvitCfg(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "img_size", "patch_size", "in_chans", "embed_dim", "depth", "num_heads", "mlp_hidden", "num_classes",
         "conv", "skip", "qkv_bias", "mlp_time_embed", "t2i", "clip_dim", "num_clip_token", "separate",
-        "enable_panoptic", "num_panoptic_class", "fp8", "fp8_linears")]
+        "enable_panoptic", "num_panoptic_class", "fp8", "fp8_linears", "residual_fp32")]
 
 
 class PdmDecoderCfg(ctypes.Structure):
@@ -58,6 +58,7 @@ class PdmGemmArgs(ctypes.Structure):
         ("w_scale_ld", ctypes.c_int), ("out_fp8", ctypes.c_void_p), ("ldo8", ctypes.c_int),
         ("out_scale", ctypes.c_void_p), ("out_scale_ld", ctypes.c_int),
         ("mx_center", ctypes.c_int), ("ln_gcol", ctypes.c_void_p),
+        ("res_in", ctypes.c_void_p), ("ldri", ctypes.c_int),
     ]
 
 
@@ -286,7 +287,7 @@ def mx_quantize_gpu(x):
 
 def gemm_ex(epi, a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=None, accumulate=False,
             ln_stats=None, ln_colsum=None, stats_out=None, out_fp8=None, out_scale=None, eps=1e-5,
-            mx_center=False, ln_gcol=None):
+            mx_center=False, ln_gcol=None, res_in=None):
     """pdm_gemm with every option (include/pdm.h pdm_gemm_args).  a / w are bf16, or float8_e4m3fn with their
     scale dword arrays (MXFP8)."""
     lib = load()
@@ -316,6 +317,8 @@ def gemm_ex(epi, a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=
         g.out_scale, g.out_scale_ld = out_scale.data_ptr(), out_scale.shape[1]
     g.mx_center = int(mx_center)
     g.ln_gcol = ln_gcol.data_ptr() if ln_gcol is not None else None
+    if res_in is not None:
+        g.res_in, g.ldri = res_in.data_ptr(), res_in.stride(0)
     check(lib.pdm_gemm(ctypes.byref(g), epi, stream_ptr(a.device)), "pdm_gemm")
 
 

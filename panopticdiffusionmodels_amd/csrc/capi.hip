@@ -80,6 +80,8 @@ struct pdm_uvit {
   // norm1 / norm2 are folded into the next Linear (fused LayerNorm, see GemmArgs): the registered
   // attn.qkv.weight / mlp.fc1.weight are W * diag(norm.weight) in bf16, ln_colsum their row sums and ln_bias
   // W norm.bias (+ the Linear's own bias), both fp32 (include/pdm.h)
+  // the residual stream is bf16 (cfg.residual_fp32 == 0; the t2i and MXFP8 forwards keep it fp32)
+  bool res16() const { return !cfg.residual_fp32 && !cfg.t2i && !cfg.fp8; }
   // block Linear `bit` (0 qkv, 1 proj, 2 fc1, 3 fc2) runs in MXFP8 (cfg.fp8 / cfg.fp8_linears)
   bool f8(int bit) const { return cfg.fp8 && (((cfg.fp8_linears ? cfg.fp8_linears : 0xF) >> bit) & 1); }
   // a block Linear's weight [N][K]: bf16, or (MXFP8) e4m3 bytes + "<key>_scale" E8M0 dwords [K/128][N]; an MXFP8
@@ -341,6 +343,71 @@ int run_block(const Ctx& c, const std::string& pre, float* X, int nseq, int L, c
   return PDM_OK;
 }
 
+// Residual GEMM on the bf16 residual stream (EPI_RES): out = bf16(A W^T + bias (+ res_in)) and its LayerNorm
+// partials (st_out).  res_in may alias out.
+int gemm_res(const Ctx& c, const bf16* A, int lda, const bf16* W, const float* bias, int M, int N, int K,
+             const bf16* res_in, bf16* out, float* st_out, const bf16* A2 = nullptr, int lda2 = 0, int K1 = 0) {
+  pdm::GemmArgs a{};
+  a.A1 = A; a.lda1 = lda;
+  a.A2 = A2; a.lda2 = lda2;
+  a.K1 = A2 ? K1 : K;
+  a.W = W; a.bias = bias;
+  a.M = M; a.N = N; a.K = K;
+  a.out_bf16 = out; a.ldo = N;
+  a.res_in = res_in; a.ldri = N; a.accumulate = res_in ? 1 : 0;
+  a.stats_out = st_out; a.stats_ld = (N + 255) / 256;
+  return launch_gemm(c, a, pdm::EPI_RES);
+}
+
+// One U-ViT Block on the bf16 residual stream (the reference under bf16 autocast keeps x in the autocast dtype:
+// each Linear's output is added to x in that dtype).  xin = the block input x (bf16) with partials st_in; the
+// block output goes to xout (may equal xin only when xin is not needed afterwards) with partials st_out.  The
+// block-internal x lives in XT.  Per residual GEMM the epilogue moves 2 + 2 bytes per element instead of the
+// fp32 stream's 4 + 4 + a 2-byte bf16 operand copy.
+int run_block16(const Ctx& c, const std::string& pre, int nseq, int L, const bf16* xin, const float* st_in,
+                const bf16* skip_in, bf16* xout, float* st_out, const Workspace& w) {
+  const pdm_uvit* h = c.h;
+  const int D = h->D, M = nseq * L;
+  const bf16* x = xin;
+  const float* st = st_in;
+  if (skip_in) {  // x = skip_linear(cat([x, skip], -1)): split-K over the two bf16 operands
+    PDM_TRY(gemm_res(c, xin, D, h->w(pre + ".skip_linear.weight"), h->f(pre + ".skip_linear.bias"), M, D, 2 * D,
+                     nullptr, w.XT, w.STT, skip_in, D, D));
+    x = w.XT;
+    st = w.STT;
+  }
+  {  // qkv = norm1(x) W^T
+    LnIO io;
+    io.st_in = st;
+    io.colsum = h->f(pre + ".attn.qkv.ln_colsum");
+    PDM_TRY(gemm(c, x, D, h->w(pre + ".attn.qkv.weight"), h->f(pre + ".attn.qkv.ln_bias"), M, 3 * D, D,
+                 pdm::EPI_BF16, w.QKV, 3 * D, nullptr, 0, 0, nullptr, 0, 0, 0, 0, io));
+  }
+  {
+    pdm::AttentionArgs a{};
+    a.qkv = w.QKV; a.ldq = 3 * D;
+    a.out = w.ATT; a.ldo = D;
+    a.B = nseq; a.L = L; a.H = h->H; a.Dh = h->Dh;
+    a.scale = 1.0f / sqrtf((float)h->Dh);
+    PDM_CHECK(pdm::attention_check(a));
+    PDM_HIP(pdm::attention_launch(a, c.s));
+  }
+  // x += proj(attn) -> XT (in place when x already is XT; xin itself may be a long-skip operand kept for later)
+  PDM_TRY(gemm_res(c, w.ATT, D, h->w(pre + ".attn.proj.weight"), h->f(pre + ".attn.proj.bias"), M, D, D, x, w.XT,
+                   w.STT));
+  {  // h = GELU(fc1(norm2(x)))
+    LnIO io;
+    io.st_in = w.STT;
+    io.colsum = h->f(pre + ".mlp.fc1.ln_colsum");
+    PDM_TRY(gemm(c, w.XT, D, h->w(pre + ".mlp.fc1.weight"), h->f(pre + ".mlp.fc1.ln_bias"), M, h->Hid, D,
+                 pdm::EPI_GELU, w.MLP, h->Hid, nullptr, 0, 0, nullptr, 0, 0, 0, 0, io));
+  }
+  // x += fc2(h) -> xout
+  PDM_TRY(gemm_res(c, w.MLP, h->Hid, h->w(pre + ".mlp.fc2.weight"), h->f(pre + ".mlp.fc2.bias"), M, D, h->Hid, w.XT,
+                   xout, st_out));
+  return PDM_OK;
+}
+
 // bf16 copy + LayerNorm partials of fp32 rows no GEMM epilogue produced (token assembly, mask-stream refresh)
 int row_stats(const Ctx& c, const float* X, int rows, bf16* xb, float* st) {
   const int D = c.h->D;
@@ -365,6 +432,25 @@ int run_stack(const Ctx& c, const Workspace& w, int rows, int L) {
     const bool last = i + 1 == h->nhalf;
     PDM_TRY(run_block(c, "out_blocks." + std::to_string(i), w.X, rows, L, w.XB, w.ST, sk, last ? nullptr : w.XB,
                       last ? nullptr : w.ST, w));
+  }
+  return PDM_OK;
+}
+
+// The block stack on the bf16 residual stream: the assembled fp32 tokens X become bf16 XB (+ partials); in-block
+// i leaves its output in SK[i] (the long skip and the next block's input); mid / out-blocks update XB.
+int run_stack16(const Ctx& c, const Workspace& w, int rows, int L) {
+  const pdm_uvit* h = c.h;
+  const size_t MD = (size_t)rows * L * h->D;
+  PDM_TRY(row_stats(c, w.X, rows * L, w.XB, w.ST));
+  const bf16* x = w.XB;
+  for (int i = 0; i < h->nhalf; ++i) {
+    PDM_TRY(run_block16(c, "in_blocks." + std::to_string(i), rows, L, x, w.ST, nullptr, w.SK + i * MD, w.ST, w));
+    x = w.SK + i * MD;
+  }
+  PDM_TRY(run_block16(c, "mid_block", rows, L, x, w.ST, nullptr, w.XB, w.ST, w));
+  for (int i = 0; i < h->nhalf; ++i) {
+    const bf16* sk = h->cfg.skip ? w.SK + (h->nhalf - 1 - i) * MD : nullptr;
+    PDM_TRY(run_block16(c, "out_blocks." + std::to_string(i), rows, L, w.XB, w.ST, sk, w.XB, w.ST, w));
   }
   return PDM_OK;
 }
@@ -497,10 +583,10 @@ int run_head(const Ctx& c, const bf16* hin, int group_stride, int row_offset, in
 // final LayerNorm over the patch tokens of X (rows extras .. L-1 of each sequence) -> HEADIN, optionally
 // adding fp32 rows `add` (use_ground_truth: libs/uvit_t2i.py:486-494) after the affine
 int final_norm(const Ctx& c, const Workspace& w, int rows, const float* X, int L, const float* add = nullptr,
-               int add_gs = 0, int add_off = 0) {
+               int add_gs = 0, int add_off = 0, const bf16* Xb = nullptr) {
   const pdm_uvit* h = c.h;
   pdm::LayerNormArgs a{};
-  a.x = X; a.ldx = h->D;
+  a.x = Xb ? nullptr : X; a.xb = Xb; a.ldx = h->D;
   a.gamma = h->f("norm.weight"); a.beta = h->f("norm.bias");
   a.y = w.HEADIN; a.ldy = h->D;
   a.rows = rows * h->n_patch; a.D = h->D;
@@ -729,8 +815,13 @@ int pdm_uvit_forward(pdm_uvit* h, const float* x, const float* t, const int64_t*
     PDM_CHECK(pdm::assemble_check(a));
     PDM_HIP(pdm::assemble_launch(a, c.s));
   }
-  PDM_TRY(h->cfg.fp8 ? run_stack8(c, w, rows, L) : run_stack(c, w, rows, L));
-  PDM_TRY(final_norm(c, w, rows, w.X, L));
+  if (h->res16()) {
+    PDM_TRY(run_stack16(c, w, rows, L));
+    PDM_TRY(final_norm(c, w, rows, nullptr, L, nullptr, 0, 0, w.XB));
+  } else {
+    PDM_TRY(h->cfg.fp8 ? run_stack8(c, w, rows, L) : run_stack(c, w, rows, L));
+    PDM_TRY(final_norm(c, w, rows, w.X, L));
+  }
   PDM_TRY(run_head(c, w.HEADIN, h->n_patch, 0, rows, "decoder_pred", h->C, h->P, h->P_pad, eps_pre));
   return PDM_OK;
 }
@@ -917,6 +1008,7 @@ int pdm_gemm(const pdm_gemm_args* g, int epi, void* stream) {
   a.out_fp8 = (unsigned char*)g->out_fp8; a.ldo8 = g->ldo8;
   a.out_scale = g->out_scale; a.out_scale_ld = g->out_scale_ld;
   a.mx_center = g->mx_center; a.ln_gcol = (const bf16*)g->ln_gcol;
+  a.res_in = (const bf16*)g->res_in; a.ldri = g->ldri;
   PDM_CHECK(pdm::gemm_check(a, epi));
   PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
   return PDM_OK;

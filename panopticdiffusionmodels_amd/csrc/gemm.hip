@@ -21,6 +21,8 @@ namespace pdm {
 
 namespace {
 constexpr int BM = 128, BN = 128, BK = 64;
+// bf16 / GELU epilogues: one bf16 output row per stored row, bias and the fused-LayerNorm consumer apply
+constexpr bool epi_rowout(int e) { return e == EPI_BF16 || e == EPI_GELU; }
 
 // A-operand row pointer for k-columns [k0, k0 + 64): dense rows, or an implicit-GEMM conv3x3 tap.
 // (b, y, x) of the row's output pixel is passed in; returns the address of element k0 of that row.
@@ -126,7 +128,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p, int tiles
   }
 
   // epilogue: lane owns rows m = .. + (lane & 15), columns n .. n+3
-  const bool ln = EPI != EPI_F32 && p.ln_stats != nullptr;
+  const bool ln = epi_rowout(EPI) && p.ln_stats != nullptr;
   float2 mr[4];
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi) {
@@ -156,6 +158,12 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p, int tiles
       } else if constexpr (EPI == EPI_GELU) {
         *reinterpret_cast<bf16x4*>(p.out_bf16 + (size_t)m * p.ldo + n) =
             to_bf16x4(gelu_act(p.act, v[0]), gelu_act(p.act, v[1]), gelu_act(p.act, v[2]), gelu_act(p.act, v[3]));
+      } else if constexpr (EPI == EPI_RES) {
+        if (p.accumulate) {
+          const bf16x4 r = *reinterpret_cast<const bf16x4*>(p.res_in + (size_t)m * p.ldri + n);
+          v += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
+        }
+        *reinterpret_cast<bf16x4*>(p.out_bf16 + (size_t)m * p.ldo + n) = to_bf16x4(v[0], v[1], v[2], v[3]);
       } else {
         f32x4* r = reinterpret_cast<f32x4*>(p.out_f32 + (size_t)m * p.ldr + n);
         if (p.accumulate) v += *r;
@@ -236,6 +244,7 @@ __device__ __forceinline__ float2 ln_from_partials(const float2 (&lst)[8], int l
 }
 
 // Epilogue of a 256x256 tile (needs 128 KiB of LDS; the staging ring is free by then).
+//  EPI_RES: the fp32 path below with a bf16 residual stream (res_in read, bf16 out_bf16 written, 16-byte rows).
 //  bf16 / GELU: the bf16 tile is written to LDS with a row-XOR chunk swizzle, then stored row-contiguously
 //    with 16-byte stores (full lines, half the store instructions of the per-lane 8-byte scatter).
 //  fp32 residual: two 128-row passes through LDS; every thread then owns 8 consecutive columns of a row:
@@ -251,14 +260,14 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
   for (int g = 0; g < 4; ++g) bv[g] = f32x4{0.f, 0.f, 0.f, 0.f};
   // cols_ready: the kernel staged the tile's bias / colsum (zeros past N or when absent) at COL_LDS in its prologue
   const float* lcol = reinterpret_cast<const float*>(smem + col_off);
-  if (EPI != EPI_F32 && cols_ready) {
+  if (epi_rowout(EPI) && cols_ready) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       int ml, nl;
       frag_pos<MAP>(MAP == 0 ? g * 8 : (g >> 1) * 8 + (g & 1) * 4, lane, wm, wn, ml, nl);
       bv[g] = *reinterpret_cast<const f32x4*>(lcol + nl);
     }
-  } else if (EPI != EPI_F32 && p.bias) {
+  } else if (epi_rowout(EPI) && p.bias) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       int ml, nl;
@@ -272,7 +281,7 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
   // area, per-column sums of the gamma-scaled weight like the bias
   float2* lnrow = reinterpret_cast<float2*>(smem + EPI_LDS);
   f32x4 cs[4];
-  const bool ln = EPI != EPI_F32 && p.ln_stats != nullptr;
+  const bool ln = epi_rowout(EPI) && p.ln_stats != nullptr;
   if (ln) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -338,6 +347,7 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
       }
     }
     if (!p.out_bf16) return;
+    if ((p.dbg_tile0 & 4) && ((n0 >> 8) & 1)) return;   // timing experiment: odd column tiles store nothing
     if (full) {
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
@@ -418,7 +428,43 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
         v0[i] = *reinterpret_cast<const f32x4*>(smem + ml * 1024 + (((2 * c8) ^ (ml & 63)) << 4)) + b0;
         v1[i] = *reinterpret_cast<const f32x4*>(smem + ml * 1024 + (((2 * c8 + 1) ^ (ml & 63)) << 4)) + b1;
       }
-      if (full) {
+      if constexpr (EPI == EPI_RES) {
+        // bf16 residual stream (GemmArgs::res_in): v += res_in, out = bf16(v); the LayerNorm partials and the MXFP8
+        // copy are taken from the rounded values (exactly what the next GEMM reads)
+        if (p.accumulate) {
+          i32x4 rr[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int idx = (g * 4 + i) * 512 + tid;
+            const int m = min(m0 + pass * 128 + (idx >> 5), p.M - 1), n = min(n0 + (idx & 31) * 8, p.N - 8);
+            rr[i] = *reinterpret_cast<const i32x4*>(p.res_in + (size_t)m * p.ldri + n);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bf16x8 r = __builtin_bit_cast(bf16x8, rr[i]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { v0[i][j] += (float)r[j]; v1[i][j] += (float)r[4 + j]; }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int idx = (g * 4 + i) * 512 + tid;
+          const int m = m0 + pass * 128 + (idx >> 5), n = n0 + (idx & 31) * 8;
+          bf16x8 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { o[j] = (bf16)v0[i][j]; o[4 + j] = (bf16)v1[i][j]; }
+          if (full || (m < p.M && n < p.N)) *reinterpret_cast<bf16x8*>(p.out_bf16 + (size_t)m * p.ldo + n) = o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v0[i][j] = (float)o[j]; v1[i][j] = (float)o[4 + j]; }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int idx = (g * 4 + i) * 512 + tid;
+          const int m = m0 + pass * 128 + (idx >> 5), n = n0 + (idx & 31) * 8;
+          const float mu = p.stats_out ? row_stats(v0[i], v1[i], m, n) : 0.f;
+          if (p.out_fp8) mx_row(v0[i], v1[i], m, n, p.mx_center ? mu : 0.f);
+        }
+      } else if (full) {
         if (p.accumulate) {
           f32x4 r0[4], r1[4];
 #pragma unroll
@@ -928,7 +974,7 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
   if (tid >= 256) {
     const int n = n0 + tid - 256;
     if (p.bias && n < p.N) cb = p.bias[n];
-    if (EPI != EPI_F32 && p.ln_stats && n < p.N) cc = p.ln_colsum[n];   // staged even when ln_D > 2048
+    if (epi_rowout(EPI) && p.ln_stats && n < p.N) cc = p.ln_colsum[n];   // staged even when ln_D > 2048
   }
   auto ln_prologue = [&]() {
     if (tid >= 256) {
@@ -1257,7 +1303,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx_kernel(GemmArgs p, int tiles_n
   // epilogue inputs fetched ahead of the first operand DMA (as gemm8d_kernel): the tile's LayerNorm row partials
   // (waves 0-3, one row each), its bias / LN column sums or, for the centred LayerNorm (GemmArgs::ln_gcol), the
   // bf16 hi / lo group sums of its columns (waves 4-7, one column each); the prologue's vmcnt wait covers them
-  const bool ln_pre = EPI != EPI_F32 && p.ln_stats != nullptr && p.ln_ld <= 8;
+  const bool ln_pre = epi_rowout(EPI) && p.ln_stats != nullptr && p.ln_ld <= 8;
   const bool lnc = ln_pre && p.ln_gcol != nullptr;
   float2 lst[8];
   if (ln_pre && tid < 256) {
@@ -1271,7 +1317,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx_kernel(GemmArgs p, int tiles_n
     const int n = n0 + tid - 256;
     if (n < p.N) {
       if (p.bias) cb = p.bias[n];
-      if (EPI != EPI_F32 && p.ln_stats && !lnc) cc = p.ln_colsum[n];
+      if (epi_rowout(EPI) && p.ln_stats && !lnc) cc = p.ln_colsum[n];
       if (lnc) {
         const i32x4* src = reinterpret_cast<const i32x4*>(p.ln_gcol + (size_t)n * 16);
         gc[0] = src[0];
@@ -1412,8 +1458,8 @@ const char* gemm_check(const GemmArgs& p, int epi) {
     if (p.conv_up && (p.convH % 2 || p.convW % 2)) return "gemm(conv): upsampled grid must be even";
   }
   if (((uintptr_t)p.A1 | (uintptr_t)p.W | (uintptr_t)(p.A2 ? p.A2 : p.A1)) & 15) return "gemm: operands must be 16-byte aligned";
-  if (p.stats_out && (epi != EPI_F32 || p.stats_ld < (p.N + 255) / 256 || ((uintptr_t)p.stats_out & 7)))
-    return "gemm: LayerNorm stats need the fp32 epilogue and stats_ld >= ceil(N / 256)";
+  if (p.stats_out && ((epi != EPI_F32 && epi != EPI_RES) || p.stats_ld < (p.N + 255) / 256 || ((uintptr_t)p.stats_out & 7)))
+    return "gemm: LayerNorm stats need the fp32 / residual epilogue and stats_ld >= ceil(N / 256)";
   if ((p.stats_out || p.ln_stats) && p.batch > 1) return "gemm: fused LayerNorm is not available for batched GEMMs";
   if (p.out_fp8 && (p.N % 32 || p.ldo8 % 16 || !p.out_scale || p.out_scale_ld < p.M || p.batch > 1 ||
                     ((uintptr_t)p.out_fp8 & 15) || ((uintptr_t)p.out_scale & 3)))
@@ -1424,18 +1470,23 @@ const char* gemm_check(const GemmArgs& p, int epi) {
     if (!p.a_scale || !p.w_scale || p.a_scale_ld < p.M || p.w_scale_ld < p.N || (p.lda1 % 16) || (p.ldw && p.ldw % 16))
       return "gemm(fp8): block scales missing or leading dimensions not multiples of 16 bytes";
   }
-  if (p.mx_center && (!p.out_fp8 || !p.stats_out || epi != EPI_F32))
+  if (p.mx_center && (!p.out_fp8 || !p.stats_out || (epi != EPI_F32 && epi != EPI_RES)))
     return "gemm: mx_center needs the fp32 epilogue with both stats_out and the MXFP8 output";
   if (p.ln_gcol && (!p.fp8 || !p.ln_stats || p.ln_ld > 8 || ((uintptr_t)p.ln_gcol & 15)))
     return "gemm: ln_gcol (centred LayerNorm) needs an MXFP8 A operand, ln_stats with ln_D <= 2048 and 16-byte alignment";
   if (p.ln_stats) {
-    if (epi == EPI_F32) return "gemm: the fused LayerNorm applies to the bf16 / GELU epilogues";
+    if (!epi_rowout(epi)) return "gemm: the fused LayerNorm applies to the bf16 / GELU epilogues";
     if (!p.ln_colsum || ((uintptr_t)p.ln_colsum & 15) || p.ln_D <= 0 || p.ln_ld != (p.ln_D + 255) / 256)
       return "gemm: fused LayerNorm needs ln_colsum and ln_ld = ceil(ln_D / 256)";
   }
   if (epi == EPI_BF16 || epi == EPI_GELU) {
     // the MXFP8 copy alone is a valid output (fc1 -> fc2 operand of the fp8 forward)
     if ((!p.out_bf16 && !p.out_fp8 && !(g_gemm_dbg & 2)) || (p.out_bf16 && p.ldo % 4)) return "gemm: bf16 output missing or ldo not a multiple of 4";
+  } else if (epi == EPI_RES) {
+    if (!p.out_bf16 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15)) return "gemm(residual): bf16 output with ldo % 8 == 0, 16-byte aligned";
+    if (p.accumulate && (!p.res_in || p.ldri % 8 || ((uintptr_t)p.res_in & 15)))
+      return "gemm(residual): accumulate needs res_in with ldri % 8 == 0, 16-byte aligned";
+    if (p.N % 8 || p.batch > 1 || p.conv) return "gemm(residual): N % 8 == 0, no batch / conv";
   } else if (epi == EPI_F32) {
     if (!p.out_f32 || (p.ldr % 4)) return "gemm: f32 output missing or ldr not a multiple of 4";
     if (p.out_bf16 && (p.ldo % 4)) return "gemm: ldo not a multiple of 4";
@@ -1499,6 +1550,8 @@ static hipError_t launch8d(const GemmArgs& p, int epi, hipStream_t stream) {
     (void)hipFuncSetAttribute((const void*)gemm8d_kernel<EPI_BF16, CONV, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     (void)hipFuncSetAttribute((const void*)gemm8d_kernel<EPI_GELU, CONV, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     (void)hipFuncSetAttribute((const void*)gemm8d_kernel<EPI_F32, CONV, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if constexpr (!CONV && SCHED == 2)
+      (void)hipFuncSetAttribute((const void*)gemm8d_kernel<EPI_RES, 0, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr_set = true;
   }
   const int tn = (p.N + BN2 - 1) / BN2, tm = (p.M + BM2 - 1) / BM2;
@@ -1507,6 +1560,12 @@ static hipError_t launch8d(const GemmArgs& p, int epi, hipStream_t stream) {
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL((gemm8d_kernel<EPI_BF16, CONV, SCHED>), grid, block, SMEM, stream, p, tn, nwg); break;
     case EPI_GELU: hipLaunchKernelGGL((gemm8d_kernel<EPI_GELU, CONV, SCHED>), grid, block, SMEM, stream, p, tn, nwg); break;
+    case EPI_RES:
+      if constexpr (!CONV && SCHED == 2) {
+        hipLaunchKernelGGL((gemm8d_kernel<EPI_RES, 0, 2>), grid, block, SMEM, stream, p, tn, nwg);
+        break;
+      }
+      return hipErrorInvalidValue;
     default: hipLaunchKernelGGL((gemm8d_kernel<EPI_F32, CONV, SCHED>), grid, block, SMEM, stream, p, tn, nwg); break;
   }
   return hipGetLastError();
@@ -1562,6 +1621,10 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
     return launch_mx(p, epi, stream);
   }
   if (p.out_fp8) algo = 7;   // MXFP8 output lives in the 256-tile epilogue
+  if (epi == EPI_RES) {      // the residual epilogue exists in the default 256-tile schedule and the 128 tile
+    if (algo != 1 && fits_rsrc(p)) return launch8d<0, 2>(p, epi, stream);
+    algo = 1;
+  }
   if (algo >= 5 && fits_rsrc(p)) {
     if (algo == 5) return p.conv ? launch8d<1, 0>(p, epi, stream) : launch8d<0, 0>(p, epi, stream);
     if (algo == 6) return p.conv ? launch8d<1, 1>(p, epi, stream) : launch8d<0, 1>(p, epi, stream);
@@ -1578,12 +1641,15 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_BF16>, grid, block, SMEM_BYTES, stream, p, tiles_n, nwg); break;
     case EPI_GELU: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_GELU>, grid, block, SMEM_BYTES, stream, p, tiles_n, nwg); break;
+    case EPI_RES: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_RES>, grid, block, SMEM_BYTES, stream, p, tiles_n, nwg); break;
     default: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_F32>, grid, block, SMEM_BYTES, stream, p, tiles_n, nwg); break;
   }
   hipError_t e = hipGetLastError();
   // the 128-tile epilogue spreads a row over two waves: its LayerNorm partials come from a row pass instead
-  if (e == hipSuccess && p.stats_out && p.batch <= 1)
-    e = rowstats_launch(p.out_f32, p.ldr, p.M, p.N, nullptr, 0, p.stats_out, p.stats_ld, stream);
+  if (e == hipSuccess && p.stats_out && p.batch <= 1) {
+    if (epi == EPI_RES) e = rowstats_bf16_launch(p.out_bf16, p.ldo, p.M, p.N, p.stats_out, p.stats_ld, stream);
+    else e = rowstats_launch(p.out_f32, p.ldr, p.M, p.N, nullptr, 0, p.stats_out, p.stats_ld, stream);
+  }
   return e;
 }
 

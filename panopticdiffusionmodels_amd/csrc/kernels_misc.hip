@@ -18,7 +18,6 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs p) {
   const int r = blockIdx.x * 4 + wave;
   if (r >= p.rows) return;
   const int src = (r / p.rows_per_group) * p.group_stride + p.row_offset + (r % p.rows_per_group);
-  const f32x4* x = reinterpret_cast<const f32x4*>(p.x + (size_t)src * p.ldx);
   const int nv = p.D >> 2;
   f32x4 v[NV];
   float s = 0.f;
@@ -26,7 +25,12 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs p) {
   for (int i = 0; i < NV; ++i) {
     const int idx = lane + i * 64;
     if (idx < nv) {
-      v[i] = x[idx];
+      if (p.xb) {   // bf16 residual stream
+        const bf16x4 b = reinterpret_cast<const bf16x4*>(p.xb + (size_t)src * p.ldx)[idx];
+        v[i] = f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+      } else {
+        v[i] = reinterpret_cast<const f32x4*>(p.x + (size_t)src * p.ldx)[idx];
+      }
       s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
     }
   }
@@ -91,6 +95,30 @@ __global__ __launch_bounds__(256) void rowstats_kernel(const float* x, int ldx, 
           reinterpret_cast<unsigned char*>(xs)[((size_t)(idx >> 5) * xs_ld + r) * 4 + ((idx >> 3) & 3)] = (unsigned char)e8;
       }
     }
+    const float q = wave_sum(ok ? (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]) : 0.f);
+    if (lane == 0) *reinterpret_cast<float2*>(stats + ((size_t)r * stats_ld + i) * 2) = make_float2(s, q);
+  }
+}
+
+// LayerNorm row partials of bf16 rows (EPI_RES outputs behind the 128-tile GEMM): one wave per row, lane l holds
+// columns 4 (l + 64 i) .. +3, so chunk i is again exactly one 256-column group
+__global__ __launch_bounds__(256) void rowstats_bf16_kernel(const bf16* x, int ldx, int rows, int D, float* stats,
+                                                            int stats_ld) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const int nv = D >> 2;
+  for (int i = 0; i * 64 < nv; ++i) {
+    const int idx = lane + i * 64;
+    const bool ok = idx < nv;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (ok) {
+      const bf16x4 b = *reinterpret_cast<const bf16x4*>(x + (size_t)r * ldx + 4 * idx);
+      v = f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+    }
+    const float s = wave_sum((v[0] + v[1]) + (v[2] + v[3]));
+    const float mu = s / (float)min(256, D - 256 * i);
+    const f32x4 d = v - mu;
     const float q = wave_sum(ok ? (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]) : 0.f);
     if (lane == 0) *reinterpret_cast<float2*>(stats + ((size_t)r * stats_ld + i) * 2) = make_float2(s, q);
   }
@@ -394,7 +422,7 @@ const char* layernorm_check(const LayerNormArgs& p) {
   if (p.D % 4 || p.D > 4 * 64 * LN_MAXV) return "layernorm: D must be a multiple of 4 and <= 2048";
   if (p.ldx % 4 || p.ldy % 4) return "layernorm: row strides must be multiples of 4";
   if (p.rows_per_group <= 0) return "layernorm: rows_per_group must be positive";
-  if (!p.x || !p.gamma || !p.beta || !p.y) return "layernorm: null pointer";
+  if ((!p.x && !p.xb) || !p.gamma || !p.beta || !p.y) return "layernorm: null pointer";
   return nullptr;
 }
 
@@ -420,6 +448,14 @@ hipError_t rowstats_launch(const float* x, int ldx, int rows, int D, bf16* xb, i
   dim3 grid((rows + 3) / 4), block(256);
   hipLaunchKernelGGL(rowstats_kernel<8>, grid, block, 0, stream, x, ldx, rows, D, xb, ldb, stats, stats_ld, xq, ldq,
                      xs, xs_ld, center);
+  return hipGetLastError();
+}
+
+hipError_t rowstats_bf16_launch(const bf16* x, int ldx, int rows, int D, float* stats, int stats_ld,
+                                hipStream_t stream) {
+  if (!x || !stats || rows <= 0 || D <= 0 || D % 4 || stats_ld < (D + 255) / 256 || ldx % 4)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rowstats_bf16_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, x, ldx, rows, D, stats, stats_ld);
   return hipGetLastError();
 }
 

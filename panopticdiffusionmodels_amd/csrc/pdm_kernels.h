@@ -10,7 +10,8 @@ namespace pdm {
 
 typedef __bf16 bf16;
 
-enum { EPI_BF16 = 0, EPI_GELU = 1, EPI_F32 = 2 };
+// EPI_RES: the residual epilogue of EPI_F32 on a bf16 residual stream: out_bf16 = bf16(acc + bias (+ res_in))
+enum { EPI_BF16 = 0, EPI_GELU = 1, EPI_F32 = 2, EPI_RES = 3 };
 
 struct GemmArgs {
   const bf16* A1; int lda1;   // A[:, 0:K1]
@@ -21,7 +22,7 @@ struct GemmArgs {
   int M, N, K;
   bf16* out_bf16; int ldo;    // EPI_BF16 / EPI_GELU output, or optional bf16 copy for EPI_F32
   float* out_f32; int ldr;    // EPI_F32 output (residual stream)
-  int accumulate;             // EPI_F32: out_f32 += result (residual add) instead of =
+  int accumulate;             // EPI_F32: out_f32 += result (residual add) instead of =; EPI_RES: add res_in
   int a_rows_per_group;       // >0: A1 row m is read from (m / rpg) * a_group_stride + m % rpg
   int a_group_stride;
   int ldw;                    // W row stride (0 -> K)
@@ -64,6 +65,9 @@ struct GemmArgs {
   //    products hi*hi + hi*lo + lo*hi (fp32-level accuracy) and ln_colsum is unused
   int mx_center;
   const bf16* ln_gcol;
+  // EPI_RES residual input [M][ldri] bf16 (may alias out_bf16: each element is read before it is written, by
+  // the same thread)
+  const bf16* res_in; int ldri;
   // tuning knobs (set by gemm_launch): raster = row panels per tile group inside an XCD's range (0: row-major);
   // dbg_tile0 = stage every tile's operands from tile (0, 0) (timing experiments only: wrong results)
   int raster, dbg_tile0;
@@ -81,6 +85,9 @@ hipError_t rowstats_launch(const float* x, int ldx, int rows, int D, bf16* xb, i
                            hipStream_t stream, unsigned char* xq = nullptr, int ldq = 0, unsigned* xs = nullptr,
                            int xs_ld = 0, int center = 0);
 
+// the same partials of bf16 rows (a bf16 residual stream: EPI_RES outputs)
+hipError_t rowstats_bf16_launch(const bf16* x, int ldx, int rows, int D, float* stats, int stats_ld, hipStream_t stream);
+
 const char* gemm_check(const GemmArgs& p, int epi);
 hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream);
 void gemm_set_algo(int algo);
@@ -89,6 +96,7 @@ void gemm_set_algo(int algo);
 // (r / rows_per_group) * group_stride + row_offset + (r % rows_per_group) of the input.
 struct LayerNormArgs {
   const float* x; int ldx;
+  const bf16* xb;             // bf16 input rows instead of x (the bf16 residual stream), same ldx
   const float* gamma; const float* beta;
   bf16* y; int ldy;
   int rows, D;

@@ -38,6 +38,7 @@ def cfg_struct(kw, t2i):
     c.num_panoptic_class = int(kw.get("num_panoptic_class", 8)) if t2i else 0
     c.fp8 = int(bool(kw.get("fp8", False)))
     c.fp8_linears = int(kw.get("fp8_linears", 0)) if c.fp8 else 0
+    c.residual_fp32 = int(kw.get("residual", "bf16") == "fp32")
     return c
 
 

@@ -209,6 +209,31 @@ def test_gemm_layernorm_producer(lib, algo, M, N, K):
     assert rel(st, _ref_partials(out)) < 1e-5
 
 
+@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("M,N,K,mode", [(4133, 1024, 1024, "inplace"), (515, 1152, 2048, "outofplace"),
+                                        (8192, 512, 256, "noacc"), (300, 264, 64, "inplace")])
+def test_gemm_residual_bf16(lib, algo, M, N, K, mode):
+    """Residual epilogue on the bf16 residual stream (EPI_RES, include/pdm.h pdm_gemm_args.res_in): out =
+    bf16(A W^T + bias + res) in place or out of place, and the LayerNorm partials of the rounded rows; vs an fp32
+    torch reference (one bf16 rounding of the sum)."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + algo + 7)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    res = (torch.randn(M, N, device="cuda", generator=g) * 3 + 2.0).bfloat16()
+    ref = a.float() @ w.float().t() + bias + (res.float() if mode != "noacc" else 0)
+    out = res.clone() if mode == "inplace" else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    st = torch.empty(M, (N + 255) // 256, 2, device="cuda")
+    lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
+    try:
+        lib.gemm_ex(lib.EPI_RES, a, w, bias, out=out, res_in=None if mode == "noacc" else (out if mode == "inplace" else res),
+                    accumulate=mode != "noacc", stats_out=st)
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+    assert rel(out.float(), ref) < 4e-3           # one bf16 rounding (2^-9) of the fp32 sum
+    assert rel(st, _ref_partials(out.float())) < 1e-5
+
+
 def test_gemm_bad_shape(lib):
     a = torch.zeros(16, 100, device="cuda", dtype=torch.bfloat16)
     w = torch.zeros(128, 100, device="cuda", dtype=torch.bfloat16)

@@ -58,6 +58,16 @@ for name, N, K, kind in shapes:
         variants["f32_acc"] = lambda: _lib.gemm_ex(_lib.EPI_F32, a, W, bias, out_f32=X, accumulate=True)
         variants["f32_acc_b_st"] = lambda: _lib.gemm_ex(_lib.EPI_F32, a, W, bias, out_f32=X, accumulate=True, out=Xb,
                                                         stats_out=st_out)
+    def tuned(dbg, fn):
+        def run():
+            lib.pdm_set_gemm_tuning(0, dbg)
+            try:
+                fn()
+            finally:
+                lib.pdm_set_gemm_tuning(0, 0)
+        return run
+    variants["nostore"] = tuned(2, lambda: _lib.gemm_ex(_lib.EPI_BF16, a, W, bias))
+    variants["halfstore"] = tuned(4, lambda: _lib.gemm_ex(_lib.EPI_BF16, a, W, bias, out=o))
     variants["hipblaslt"] = lambda: torch.nn.functional.linear(a, W)
     line = f"{name:5s} M={M} N={N} K={K}"
     for k, fn in variants.items():
