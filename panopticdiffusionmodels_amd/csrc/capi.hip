@@ -80,8 +80,8 @@ struct pdm_uvit {
   // norm1 / norm2 are folded into the next Linear (fused LayerNorm, see GemmArgs): the registered
   // attn.qkv.weight / mlp.fc1.weight are W * diag(norm.weight) in bf16, ln_colsum their row sums and ln_bias
   // W norm.bias (+ the Linear's own bias), both fp32 (include/pdm.h)
-  // the residual stream is bf16 (cfg.residual_fp32 == 0; the t2i and MXFP8 forwards keep it fp32)
-  bool res16() const { return !cfg.residual_fp32 && !cfg.t2i && !cfg.fp8; }
+  // the residual stream is bf16 (cfg.residual_fp32 == 0)
+  bool res16() const { return !cfg.residual_fp32; }
   // block Linear `bit` (0 qkv, 1 proj, 2 fc1, 3 fc2) runs in MXFP8 (cfg.fp8 / cfg.fp8_linears)
   bool f8(int bit) const { return cfg.fp8 && (((cfg.fp8_linears ? cfg.fp8_linears : 0xF) >> bit) & 1); }
   // a block Linear's weight [N][K]: bf16, or (MXFP8) e4m3 bytes + "<key>_scale" E8M0 dwords [K/128][N]; an MXFP8
@@ -144,6 +144,7 @@ struct Workspace {
   float* MX;    // [rows*Lm, D] mask stream
   bf16* MXB;    // [rows*Lm, D] bf16 copy of the mask-stream block output
   bf16* MXIN;   // [rows*Lm, D] bf16 copy of the mask-stream block input (qkv / skip_linear operand)
+  bf16* MB;     // [rows*Lm, D] bf16 mask-stream block input (bf16 residual stream: MX is then only assembly scratch)
   bf16* SKM;    // [nhalf][rows*Lm, D]
   float* STM;   // [rows*Lm, T] LayerNorm partials of the mask stream
   // fp8 forward (cfg.fp8): MXFP8 operands of the block Linears, e4m3 rows + E8M0 scale dwords [K/128][rows*Lx]
@@ -171,7 +172,7 @@ Workspace layout(const pdm_uvit* h, int rows, char* base) {
   const bool f8 = h->cfg.fp8 != 0;   // MXFP8 operands replace XT / MLP; XB / SK stay (bf16 skip_linear)
   w.X = (float*)take(Mx * D * 4);
   w.XB = (bf16*)take(Mx * D * 2);
-  if (!f8 || !h->f8(2)) w.XT = (bf16*)take(Mmax * D * 2);   // (fp8 with a bf16 fc1: its A operand)
+  if (!f8 || !h->f8(2) || h->res16()) w.XT = (bf16*)take(Mmax * D * 2);   // (fp8: bf16 fc1 operand / bf16 stream)
   w.ST = (float*)take(Mmax * T * 8);
   w.STT = (float*)take(Mmax * T * 8);
   w.QKV = (bf16*)take(Mmax * 3 * D * 2);
@@ -198,6 +199,7 @@ Workspace layout(const pdm_uvit* h, int rows, char* base) {
     w.CTXB = (bf16*)take((size_t)rows * h->cfg.num_clip_token * h->cfg.clip_dim * 2);
   }
   if (mask) {
+    if (h->res16()) w.MB = (bf16*)take(Mm * D * 2);
     w.MX = (float*)take(Mm * D * 4);
     w.MXB = (bf16*)take(Mm * D * 2);
     w.MXIN = (bf16*)take(Mm * D * 2);
@@ -259,8 +261,9 @@ int gemm(const Ctx& c, const bf16* A, int lda, const bf16* W, const float* bias,
 // epilogue also writes the MXFP8 copy of what it stores into `out` when out.q is set (the next Linear's operand)
 // LayerNorm consumers (ln.st_in) take their A operand group-centred (GemmArgs::ln_gcol, "<lin>.ln_gcol"); an
 // MXFP8 output written beside LayerNorm partials (ln.st_out) is group-centred (GemmArgs::mx_center).
+// epi == EPI_RES: the bf16 residual stream, res_in (may alias ob) added when accumulate.
 int gemm8(const Ctx& c, const Q8& A, const std::string& wkey, const float* bias, int M, int N, int K, int epi,
-          bf16* ob, float* of, int accumulate, LnIO ln, const Q8& out) {
+          bf16* ob, float* of, int accumulate, LnIO ln, const Q8& out, const bf16* res_in = nullptr) {
   const pdm_uvit* h = c.h;
   pdm::GemmArgs a{};
   const int T = (h->D + 255) / 256;
@@ -277,6 +280,7 @@ int gemm8(const Ctx& c, const Q8& A, const std::string& wkey, const float* bias,
   a.a_scale = A.s; a.a_scale_ld = A.sld;
   a.w_scale = (const unsigned*)h->ptr(wkey + "_scale"); a.w_scale_ld = N;
   a.out_fp8 = out.q; a.ldo8 = out.ld; a.out_scale = out.s; a.out_scale_ld = out.sld;
+  a.res_in = res_in; a.ldri = res_in ? N : 0;
   return launch_gemm(c, a, epi);
 }
 
@@ -463,24 +467,31 @@ int run_stack16(const Ctx& c, const Workspace& w, int rows, int L) {
 // 72-deep QK^T cannot fill the 128-deep scaled MFMA, and the unscaled fp8 MFMA runs at the bf16 rate); its output
 // is MX-quantised for proj.  fc2 leaves the block output as MXFP8 in out8 and / or bf16 in outb (either may be
 // null) and its partials in st_out.
+//
+// X == nullptr: the bf16 residual stream (cfg.residual_fp32 == 0): xb_in is the block input x itself (bf16), the
+// residual epilogues are EPI_RES, the block-internal x lives in XT and the block output goes to outb (required).
 int run_block8(const Ctx& c, const std::string& pre, float* X, int M, int L, const Q8& in, const float* st_in,
                const bf16* xb_in, const bf16* skip_in, const Q8& out8, bf16* outb, float* st_out, const Workspace& w) {
   const pdm_uvit* h = c.h;
   const int D = h->D;
+  const bool r16 = X == nullptr;
   Q8 a = in;
   const float* st = st_in;
-  if (skip_in) {  // x = skip_linear(cat([x, skip], -1)) -> X (fp32) + its MXFP8 copy (qkv operand) + partials
+  const bf16* res = xb_in;   // (r16) the residual x the block adds to
+  if (skip_in) {  // x = skip_linear(cat([x, skip], -1)) -> X (fp32) / XT (bf16) + its MXFP8 copy (qkv operand) + partials
     pdm::GemmArgs g{};
     g.A1 = xb_in; g.lda1 = D; g.A2 = skip_in; g.lda2 = D; g.K1 = D;
     g.W = h->w(pre + ".skip_linear.weight"); g.bias = h->f(pre + ".skip_linear.bias");
     g.M = M; g.N = D; g.K = 2 * D;
-    g.out_f32 = X; g.ldr = D;
+    if (r16) { g.out_bf16 = w.XT; g.ldo = D; }
+    else { g.out_f32 = X; g.ldr = D; }
     g.stats_out = w.STT; g.stats_ld = (D + 255) / 256;
     g.out_fp8 = w.xtq.q; g.ldo8 = w.xtq.ld; g.out_scale = w.xtq.s; g.out_scale_ld = w.xtq.sld;
     g.mx_center = 1;
-    PDM_TRY(launch_gemm(c, g, pdm::EPI_F32));
+    PDM_TRY(launch_gemm(c, g, r16 ? pdm::EPI_RES : pdm::EPI_F32));
     a = w.xtq;
     st = w.STT;
+    res = w.XT;
   }
   {  // qkv = norm1(x) W^T (bf16 for the attention kernel)
     LnIO io;
@@ -500,11 +511,15 @@ int run_block8(const Ctx& c, const std::string& pre, float* X, int M, int L, con
     PDM_HIP(pdm::mxq_launch(w.ATT, 1, D, M, D, w.atq.q, w.atq.ld, w.atq.s, w.atq.sld, c.s));
   }
   const bool fc1_8 = h->f8(2);
-  {  // x += proj(attn) -> X, its partials and the fc1 operand (centred MXFP8, or bf16 for a bf16 fc1)
+  {  // x += proj(attn) -> X / XT, its partials and the fc1 operand (centred MXFP8, or bf16 for a bf16 fc1)
     LnIO io;
     io.st_out = w.STT;
-    PDM_TRY(gemm8(c, w.atq, pre + ".attn.proj.weight", h->f(pre + ".attn.proj.bias"), M, D, D, pdm::EPI_F32,
-                  fc1_8 ? nullptr : w.XT, X, 1, io, fc1_8 ? w.xtq : Q8()));
+    if (r16)
+      PDM_TRY(gemm8(c, w.atq, pre + ".attn.proj.weight", h->f(pre + ".attn.proj.bias"), M, D, D, pdm::EPI_RES, w.XT,
+                    nullptr, 1, io, fc1_8 ? w.xtq : Q8(), res));
+    else
+      PDM_TRY(gemm8(c, w.atq, pre + ".attn.proj.weight", h->f(pre + ".attn.proj.bias"), M, D, D, pdm::EPI_F32,
+                    fc1_8 ? nullptr : w.XT, X, 1, io, fc1_8 ? w.xtq : Q8()));
   }
   {  // h = GELU(fc1(norm2(x))), stored only as the MXFP8 fc2 operand
     LnIO io;
@@ -527,9 +542,37 @@ int run_block8(const Ctx& c, const std::string& pre, float* X, int M, int L, con
   {  // x += fc2(h)
     LnIO io;
     io.st_out = st_out;
-    PDM_TRY(gemm8(c, w.mlq, pre + ".mlp.fc2.weight", h->f(pre + ".mlp.fc2.bias"), M, D, h->Hid, pdm::EPI_F32, outb,
-                  X, 1, io, out8));
+    if (r16)
+      PDM_TRY(gemm8(c, w.mlq, pre + ".mlp.fc2.weight", h->f(pre + ".mlp.fc2.bias"), M, D, h->Hid, pdm::EPI_RES, outb,
+                    nullptr, 1, io, out8, w.XT));
+    else
+      PDM_TRY(gemm8(c, w.mlq, pre + ".mlp.fc2.weight", h->f(pre + ".mlp.fc2.bias"), M, D, h->Hid, pdm::EPI_F32, outb,
+                    X, 1, io, out8));
   }
+  return PDM_OK;
+}
+
+// run_stack8 on the bf16 residual stream: in-block i leaves x in SK[i] (bf16: the long skip and the next block's
+// residual) and MXFP8 xq (the next qkv operand); the mid / out-blocks update XB.
+int run_stack8_16(const Ctx& c, const Workspace& w, int rows, int L) {
+  const pdm_uvit* h = c.h;
+  const int D = h->D, M = rows * L, n = h->nhalf;
+  const bool skip = h->cfg.skip != 0;
+  const size_t MD = (size_t)M * D;
+  PDM_HIP(pdm::rowstats_launch(w.X, D, M, D, w.XB, D, w.ST, (D + 255) / 256, c.s, w.xq.q, w.xq.ld, w.xq.s,
+                               w.xq.sld, 1));
+  // a block reads its input x (skip_linear or proj) before fc2 writes the output, so XB can be updated in place;
+  // in-block outputs with long skips are kept in SK[i]
+  const bf16* x = w.XB;
+  for (int i = 0; i < n; ++i) {
+    bf16* o = skip ? w.SK + i * MD : w.XB;
+    PDM_TRY(run_block8(c, "in_blocks." + std::to_string(i), nullptr, M, L, w.xq, w.ST, x, nullptr, w.xq, o, w.ST, w));
+    x = o;
+  }
+  PDM_TRY(run_block8(c, "mid_block", nullptr, M, L, w.xq, w.ST, x, nullptr, skip ? Q8() : w.xq, w.XB, w.ST, w));
+  for (int i = 0; i < n; ++i)
+    PDM_TRY(run_block8(c, "out_blocks." + std::to_string(i), nullptr, M, L, w.xq, w.ST, w.XB,
+                       skip ? w.SK + (n - 1 - i) * MD : nullptr, skip ? Q8() : w.xq, w.XB, w.ST, w));
   return PDM_OK;
 }
 
@@ -583,10 +626,11 @@ int run_head(const Ctx& c, const bf16* hin, int group_stride, int row_offset, in
 // final LayerNorm over the patch tokens of X (rows extras .. L-1 of each sequence) -> HEADIN, optionally
 // adding fp32 rows `add` (use_ground_truth: libs/uvit_t2i.py:486-494) after the affine
 int final_norm(const Ctx& c, const Workspace& w, int rows, const float* X, int L, const float* add = nullptr,
-               int add_gs = 0, int add_off = 0, const bf16* Xb = nullptr) {
+               int add_gs = 0, int add_off = 0, const bf16* Xb = nullptr, const bf16* addb = nullptr) {
   const pdm_uvit* h = c.h;
   pdm::LayerNormArgs a{};
   a.x = Xb ? nullptr : X; a.xb = Xb; a.ldx = h->D;
+  a.addb = addb;
   a.gamma = h->f("norm.weight"); a.beta = h->f("norm.bias");
   a.y = w.HEADIN; a.ldy = h->D;
   a.rows = rows * h->n_patch; a.D = h->D;
@@ -595,6 +639,82 @@ int final_norm(const Ctx& c, const Workspace& w, int rows, const float* X, int L
   a.add = add; a.add_ld = h->D; a.add_group_stride = add_gs; a.add_row_offset = add_off;
   PDM_CHECK(pdm::layernorm_check(a));
   PDM_HIP(pdm::layernorm_launch(a, c.s));
+  return PDM_OK;
+}
+
+// The panoptic two-stream U-ViT (libs/uvit_t2i.py:411-525) on the bf16 residual stream, after the image tokens
+// (X) and the mask tokens (MX[:, Lx:]) were assembled in fp32.  Per layer: the mask stream input mb = cat(x, m)
+// is rebuilt in MB (image rows copied from the image block's INPUT x, 426 / 443 / 459; mask rows from the
+// previous mask block's output), both blocks run, then x += zeroconv(mask block output[:, :Lx]) (435-436,
+// 452-453, 470-472) as a residual GEMM into the image output buffer.
+int t2i_two_stream16(const Ctx& c, const Workspace& w, int rows, int use_ground_truth, float* eps_pre,
+                     float* mask_pre) {
+  const pdm_uvit* h = c.h;
+  const int D = h->D, Lx = h->Lx, Lm = h->Lm, n = h->nhalf, T = (D + 255) / 256;
+  const size_t MDx = (size_t)rows * Lx * D, MDm = (size_t)rows * Lm * D;
+  // bf16 row copies of D columns (as fp32 words: D / 2 per row)
+  auto copy_rows = [&](bf16* dst, const bf16* src, int rpg, int dgs, int sgs) -> int {
+    PDM_HIP(pdm::rowcopy_launch((float*)dst, D / 2, (const float*)src, D / 2, rows * rpg, D / 2, rpg, dgs, sgs, c.s));
+    return PDM_OK;
+  };
+  // mb = cat(x_img, m_src[:, Lx:]) + its partials (m_src == MB: the mask rows are already in place)
+  auto refresh = [&](const bf16* x_img, const bf16* m_src) -> int {
+    PDM_TRY(copy_rows(w.MB, x_img, Lx, Lm, Lx));
+    if (m_src != w.MB) PDM_TRY(copy_rows(w.MB + (size_t)Lx * D, m_src + (size_t)Lx * D, Lm - Lx, Lm, Lm));
+    PDM_HIP(pdm::rowstats_bf16_launch(w.MB, D, rows * Lm, D, w.STM, T, c.s));
+    return PDM_OK;
+  };
+  auto inject = [&](int layer, const bf16* mout, const bf16* x_res, bf16* x_out) -> int {
+    const std::string zc = "zero_convs." + std::to_string(2 * layer + 1) + ".conv";
+    pdm::GemmArgs a{};
+    a.A1 = mout; a.lda1 = D; a.K1 = D;
+    a.a_rows_per_group = Lx; a.a_group_stride = Lm;
+    a.W = h->w(zc + ".weight"); a.bias = h->f(zc + ".bias");
+    a.M = rows * Lx; a.N = D; a.K = D;
+    a.out_bf16 = x_out; a.ldo = D;
+    a.res_in = x_res; a.ldri = D; a.accumulate = 1;
+    a.stats_out = w.ST; a.stats_ld = T;
+    return launch_gemm(c, a, pdm::EPI_RES);
+  };
+  // image tokens -> XB + ST; mask tokens -> MB[:, Lx:] (the image rows of this pass are overwritten by refresh)
+  PDM_TRY(row_stats(c, w.X, rows * Lx, w.XB, w.ST));
+  PDM_TRY(row_stats(c, w.MX, rows * Lm, w.MB, w.STM));
+  const bf16* x = w.XB;
+  const bf16* m = w.MB;
+  int layer = 0;
+  // Per layer the mask block runs first (its input only needs the image block's INPUT x), then the image block,
+  // whose output stays in XT (its proj / fc2 update XT in place), then the injection writes the layer's x.  The
+  // blocks' own output partials are not needed: the injection and the next refresh produce them.
+  for (int i = 0; i < n; ++i, ++layer) {
+    PDM_TRY(refresh(x, m));
+    PDM_TRY(run_block16(c, "in_blocks_mask." + std::to_string(i), rows, Lm, w.MB, w.STM, nullptr, w.SKM + i * MDm,
+                        nullptr, w));
+    PDM_TRY(run_block16(c, "in_blocks." + std::to_string(i), rows, Lx, x, w.ST, nullptr, w.XT, nullptr, w));
+    PDM_TRY(inject(layer, w.SKM + i * MDm, w.XT, w.SK + i * MDx));
+    x = w.SK + i * MDx;
+    m = w.SKM + i * MDm;
+  }
+  PDM_TRY(refresh(x, m));
+  PDM_TRY(run_block16(c, "mid_block_mask", rows, Lm, w.MB, w.STM, nullptr, w.MXB, nullptr, w));
+  PDM_TRY(run_block16(c, "mid_block", rows, Lx, x, w.ST, nullptr, w.XT, nullptr, w));
+  PDM_TRY(inject(layer, w.MXB, w.XT, w.XB));
+  ++layer;
+  for (int i = 0; i < n; ++i, ++layer) {
+    PDM_TRY(refresh(w.XB, w.MXB));
+    const bf16* skm = h->cfg.skip ? w.SKM + (n - 1 - i) * MDm : nullptr;
+    PDM_TRY(run_block16(c, "out_blocks_mask." + std::to_string(i), rows, Lm, w.MB, w.STM, skm, w.MXB, nullptr, w));
+    const bf16* sk = h->cfg.skip ? w.SK + (n - 1 - i) * MDx : nullptr;
+    PDM_TRY(run_block16(c, "out_blocks." + std::to_string(i), rows, Lx, w.XB, w.ST, sk, w.XT, nullptr, w));
+    PDM_TRY(inject(layer, w.MXB, w.XT, w.XB));
+  }
+  // heads (477-519): noise from norm(x) patch tokens; mask head on the un-normalised m (the last mask output)
+  if (use_ground_truth) {
+    PDM_TRY(final_norm(c, w, rows, nullptr, Lx, nullptr, Lm, Lx, w.XB, w.MXB));
+  } else {
+    PDM_TRY(final_norm(c, w, rows, nullptr, Lx, nullptr, 0, 0, w.XB));
+    PDM_TRY(run_head(c, w.MXB, Lm, Lx, rows, "decoder_pred_mask", h->K, h->PK, h->PK_pad, mask_pre));
+  }
+  PDM_TRY(run_head(c, w.HEADIN, h->n_patch, 0, rows, "decoder_pred", h->C, h->P, h->P_pad, eps_pre));
   return PDM_OK;
 }
 
@@ -816,7 +936,7 @@ int pdm_uvit_forward(pdm_uvit* h, const float* x, const float* t, const int64_t*
     PDM_HIP(pdm::assemble_launch(a, c.s));
   }
   if (h->res16()) {
-    PDM_TRY(run_stack16(c, w, rows, L));
+    PDM_TRY(h->cfg.fp8 ? run_stack8_16(c, w, rows, L) : run_stack16(c, w, rows, L));
     PDM_TRY(final_norm(c, w, rows, nullptr, L, nullptr, 0, 0, w.XB));
   } else {
     PDM_TRY(h->cfg.fp8 ? run_stack8(c, w, rows, L) : run_stack(c, w, rows, L));
@@ -857,8 +977,13 @@ int pdm_uvit_t2i_forward(pdm_uvit* h, const float* x, const float* t, const floa
   }
   const size_t MDx = (size_t)rows * Lx * D;
   if (!two) {  // plain text-conditioned U-ViT (mask_token None: 407-410, 516-517)
-    PDM_TRY(run_stack(c, w, rows, Lx));
-    PDM_TRY(final_norm(c, w, rows, w.X, Lx));
+    if (h->res16()) {
+      PDM_TRY(run_stack16(c, w, rows, Lx));
+      PDM_TRY(final_norm(c, w, rows, nullptr, Lx, nullptr, 0, 0, w.XB));
+    } else {
+      PDM_TRY(run_stack(c, w, rows, Lx));
+      PDM_TRY(final_norm(c, w, rows, w.X, Lx));
+    }
     PDM_TRY(run_head(c, w.HEADIN, h->n_patch, 0, rows, "decoder_pred", h->C, h->P, h->P_pad, eps_pre));
     return PDM_OK;
   }
@@ -873,6 +998,7 @@ int pdm_uvit_t2i_forward(pdm_uvit* h, const float* x, const float* t, const floa
     PDM_HIP(pdm::assemble_launch(a, c.s));
   }
   const size_t MDm = (size_t)rows * Lm * D;
+  if (h->res16()) return t2i_two_stream16(c, w, rows, use_ground_truth, eps_pre, mask_pre);
   // mx = cat(x, m): refresh the image half of the mask stream before every mask block (426, 443, 459), then
   // the bf16 copy + LayerNorm partials of the whole mask stream (its blocks' qkv / skip_linear operand)
   auto refresh = [&]() -> int {

@@ -1442,6 +1442,8 @@ __global__ __launch_bounds__(512, 1) void gemm_mx_kernel(GemmArgs p, int tiles_n
 
 static int g_gemm_raster = 0, g_gemm_dbg = 0;   // tuning knobs (pdm_set_gemm_tuning)
 
+static bool fits_rsrc(const GemmArgs& p);
+
 const char* gemm_check(const GemmArgs& p, int epi) {
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return "gemm: M, N, K must be positive";
   if (p.N % 4) return "gemm: N must be a multiple of 4";
@@ -1469,6 +1471,8 @@ const char* gemm_check(const GemmArgs& p, int epi) {
       return "gemm(fp8): K must be a multiple of 128; no split-K, conv, row gather or batch";
     if (!p.a_scale || !p.w_scale || p.a_scale_ld < p.M || p.w_scale_ld < p.N || (p.lda1 % 16) || (p.ldw && p.ldw % 16))
       return "gemm(fp8): block scales missing or leading dimensions not multiples of 16 bytes";
+    if (!fits_rsrc(p))
+      return "gemm(fp8): an operand spans >= 2 GiB (32-bit buffer offsets); split M into smaller launches";
   }
   if (p.mx_center && (!p.out_fp8 || !p.stats_out || (epi != EPI_F32 && epi != EPI_RES)))
     return "gemm: mx_center needs the fp32 epilogue with both stats_out and the MXFP8 output";
@@ -1577,6 +1581,7 @@ static hipError_t launch_mx(const GemmArgs& p, int epi, hipStream_t stream) {
     (void)hipFuncSetAttribute((const void*)gemm_mx_kernel<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, MX_SMEM);
     (void)hipFuncSetAttribute((const void*)gemm_mx_kernel<EPI_GELU>, hipFuncAttributeMaxDynamicSharedMemorySize, MX_SMEM);
     (void)hipFuncSetAttribute((const void*)gemm_mx_kernel<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, MX_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm_mx_kernel<EPI_RES>, hipFuncAttributeMaxDynamicSharedMemorySize, MX_SMEM);
     attr_set = true;
   }
   const int tn = (p.N + BN2 - 1) / BN2, tm = (p.M + BM2 - 1) / BM2;
@@ -1585,6 +1590,7 @@ static hipError_t launch_mx(const GemmArgs& p, int epi, hipStream_t stream) {
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL(gemm_mx_kernel<EPI_BF16>, grid, block, MX_SMEM, stream, p, tn, nwg); break;
     case EPI_GELU: hipLaunchKernelGGL(gemm_mx_kernel<EPI_GELU>, grid, block, MX_SMEM, stream, p, tn, nwg); break;
+    case EPI_RES: hipLaunchKernelGGL(gemm_mx_kernel<EPI_RES>, grid, block, MX_SMEM, stream, p, tn, nwg); break;
     default: hipLaunchKernelGGL(gemm_mx_kernel<EPI_F32>, grid, block, MX_SMEM, stream, p, tn, nwg); break;
   }
   return hipGetLastError();
@@ -1593,13 +1599,14 @@ static hipError_t launch_mx(const GemmArgs& p, int epi, hipStream_t stream) {
 // The descriptor-addressed kernel needs every operand byte offset below 2^31 (32-bit per-lane offsets).
 static bool fits_rsrc(const GemmArgs& p) {
   const long long lim = 0x7fffffffLL;
+  const long long es = p.fp8 ? 1 : 2;   // operand bytes per element (MXFP8 rows are e4m3 bytes)
   long long a1;
   if (p.conv) a1 = (long long)(p.M / (p.convH * p.convW)) * (p.convH >> p.conv_up) * (p.convW >> p.conv_up) * p.convC * 2;
   else if (p.a_rows_per_group > 0)
-    a1 = ((long long)((p.M - 1) / p.a_rows_per_group) * p.a_group_stride + p.a_rows_per_group) * p.lda1 * 2;
-  else a1 = (long long)p.M * p.lda1 * 2;
+    a1 = ((long long)((p.M - 1) / p.a_rows_per_group) * p.a_group_stride + p.a_rows_per_group) * p.lda1 * es;
+  else a1 = (long long)p.M * p.lda1 * es;
   const long long a2 = p.A2 ? (long long)p.M * p.lda2 * 2 : 0;
-  const long long w = (long long)p.N * (p.ldw > 0 ? p.ldw : p.K) * 2;
+  const long long w = (long long)p.N * (p.ldw > 0 ? p.ldw : p.K) * es;
   return a1 < lim && a2 < lim && w < lim && (!p.conv || p.convW < 4096);
 }
 

@@ -49,9 +49,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs p) {
   const f32x4* bt = reinterpret_cast<const f32x4*>(p.beta);
   bf16x4* y = reinterpret_cast<bf16x4*>(p.y + (size_t)r * p.ldy);
   const f32x4* ad = nullptr;
-  if (p.add) {
+  const bf16x4* adb = nullptr;
+  if (p.add || p.addb) {
     const int arow = (r / p.rows_per_group) * p.add_group_stride + p.add_row_offset + (r % p.rows_per_group);
-    ad = reinterpret_cast<const f32x4*>(p.add + (size_t)arow * p.add_ld);
+    if (p.addb) adb = reinterpret_cast<const bf16x4*>(p.addb + (size_t)arow * p.add_ld);
+    else ad = reinterpret_cast<const f32x4*>(p.add + (size_t)arow * p.add_ld);
   }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -59,6 +61,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LayerNormArgs p) {
     if (idx < nv) {
       f32x4 o = (v[i] - mean) * rstd * gm[idx] + bt[idx];
       if (ad) o += ad[idx];
+      if (adb) {
+        const bf16x4 b = adb[idx];
+        o += f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+      }
       y[idx] = to_bf16x4(o[0], o[1], o[2], o[3]);
     }
   }

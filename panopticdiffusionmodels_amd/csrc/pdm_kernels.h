@@ -103,6 +103,7 @@ struct LayerNormArgs {
   int rows_per_group, group_stride, row_offset;   // row gather (final norm over patch tokens only)
   float eps;
   const float* add;           // optional fp32 rows added after the affine (gathered like x, with add_* below)
+  const bf16* addb;           // the same rows in bf16 (the bf16 residual stream), instead of add
   int add_ld, add_group_stride, add_row_offset;
 };
 const char* layernorm_check(const LayerNormArgs& p);

@@ -78,7 +78,6 @@ class UViT(HipNet):
                  use_checkpoint=False, conv=True, skip=True):
         super().__init__()
         self.precision = "bf16"
-        self.residual = "bf16"
         if qk_scale is not None:
             raise ValueError("qk_scale other than the default head_dim ** -0.5 is not supported")
         self.num_features = self.embed_dim = embed_dim
@@ -113,16 +112,6 @@ class UViT(HipNet):
                     num_classes=self.num_classes, conv=self.conv, skip=self.skip, qkv_bias=self.qkv_bias,
                     mlp_time_embed=self.mlp_time_embed, fp8=self.precision != "bf16",
                     fp8_linears=self.FP8_LINEARS[self.precision], residual=self.residual)
-
-    def set_residual(self, dtype):
-        """Precision of the residual stream x between the block Linears: 'bf16' (default: the reference's GPU
-        run under autocast adds every Linear output to x in the autocast dtype) or 'fp32' (include/pdm.h
-        pdm_uvit_cfg.residual_fp32).  The MXFP8 forward keeps fp32.  Re-packs the handle."""
-        if dtype not in ("bf16", "fp32"):
-            raise ValueError(f"residual must be 'bf16' or 'fp32', got {dtype!r}")
-        self.residual = dtype
-        self.invalidate()
-        return self
 
     # include/pdm.h pdm_uvit_cfg.fp8_linears: bit 0 attn.qkv, 1 attn.proj, 2 mlp.fc1, 3 mlp.fc2
     FP8_LINEARS = {"bf16": 0, "fp8": 0xB, "fp8-all": 0xF}

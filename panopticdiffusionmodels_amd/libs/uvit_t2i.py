@@ -86,7 +86,7 @@ class UViT(HipNet):
                     conv=self.conv, skip=self.skip, qkv_bias=self.qkv_bias, mlp_time_embed=self.mlp_time_embed,
                     clip_dim=self.clip_dim, num_clip_token=self.num_clip_token, separate=self.separate,
                     enable_panoptic=self.enable_panoptic,
-                    num_panoptic_class=getattr(self, "num_panoptic_class", 8))
+                    num_panoptic_class=getattr(self, "num_panoptic_class", 8), residual=self.residual)
 
     @torch.jit.ignore
     def no_weight_decay(self):

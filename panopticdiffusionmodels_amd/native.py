@@ -195,6 +195,17 @@ class HipNet(nn.Module):
         super().__init__()
         self._native = None
         self._generation = 0
+        self.residual = "bf16"
+
+    def set_residual(self, dtype):
+        """Precision of the residual stream x between the block Linears: 'bf16' (default: the reference's GPU
+        run under autocast adds every Linear output to x in the autocast dtype) or 'fp32' (include/pdm.h
+        pdm_uvit_cfg.residual_fp32).  Re-packs the handle."""
+        if dtype not in ("bf16", "fp32"):
+            raise ValueError(f"residual must be 'bf16' or 'fp32', got {dtype!r}")
+        self.residual = dtype
+        self.invalidate()
+        return self
 
     def _native_cfg_kwargs(self):
         raise NotImplementedError

@@ -105,7 +105,8 @@ def dev():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,residual", [(n, "bf16") for n in FWD] + [("imagenet256_uvit_large", "fp32")])
+@pytest.mark.parametrize("name,residual", [(n, "bf16") for n in FWD] + [("imagenet256_uvit_large", "fp32"),
+                                                                         ("mscoco_uvit_small", "fp32")])
 def test_hip_vs_reference_fullsize_forward(fs, dev, name, residual):
     """residual: the stream x between the block Linears in bf16 (default, as the reference's autocast run) or
     fp32 (libs/uvit.py UViT.set_residual)."""
