@@ -102,7 +102,7 @@ def main():
     if t2i:   # configs[3]: prompts -> CLIP contexts (sample_t2i_discrete.py:49-53) -> panoptic co-generation
         from panopticdiffusionmodels_amd.libs.clip import FrozenCLIPEmbedder
         from panopticdiffusionmodels_amd.sampler import T2ISampler
-        clip = FrozenCLIPEmbedder()
+        clip = FrozenCLIPEmbedder(synthetic=True)
         with torch.no_grad():   # seeded synthetic ViT-L/14 text weights (no checkpoint offline)
             g = torch.Generator().manual_seed(5)
             for k, v in clip.transformer.state_dict().items():

@@ -89,7 +89,9 @@ int pdm_uvit_create(const pdm_uvit_cfg* cfg, pdm_uvit** out);
 int pdm_uvit_destroy(pdm_uvit* h);
 /* replaces load_state_dict (eval_ldm_discrete.py:46): register the device address of one packed weight
  * under its reference state_dict key.  Linear weights bf16 [out, in]; everything
- * else fp32.  decoder_pred(.mask).weight is bf16 padded to a multiple of 16 rows. */
+ * else fp32.  decoder_pred(.mask).weight is bf16 padded to a multiple of 16 rows.  attn.qkv (weight,
+ * ln_colsum, ln_bias) is norm1-folded and its q rows (0 .. embed_dim) are scaled by Dh^-0.5 * log2(e), the
+ * softmax scale in base 2 (libs/uvit.py:64,73): the attention kernels then exponentiate the scores directly. */
 int pdm_uvit_set_param(pdm_uvit* h, const char* name, const void* dev_ptr, int dtype, long long numel);
 /* enumerate the keys the handle expects (name, dtype, element count) */
 int pdm_uvit_param_count(const pdm_uvit* h);
@@ -207,6 +209,9 @@ int pdm_layernorm(const float* x, int ldx, const float* gamma, const float* beta
 /* Attention core (libs/uvit.py:66-92 minus the two Linears): packed qkv bf16 -> bf16 */
 int pdm_attention(const void* qkv, int ldq, void* out, int ldo, int B, int L, int H, int Dh, float scale,
                   void* stream);
+/* the same with q already multiplied by Dh^-0.5 * log2(e) (what the U-ViT forward's qkv GEMM produces: its
+ * attn.qkv q rows are packed pre-scaled), so the softmax is taken as exp2 of the scores directly */
+int pdm_attention_log2(const void* qkv, int ldq, void* out, int ldo, int B, int L, int H, int Dh, void* stream);
 /* fp32 -> bf16 conversion (round to nearest even); n == 0 is a no-op (null pointers allowed) */
 int pdm_f32_to_bf16(const float* x, void* y, long long n, void* stream);
 /* MXFP8 quantisation of rows x [rows][ldx] (dtype PDM_F32 or PDM_BF16, K % 32 == 0) -> e4m3 q [rows][ldq] and

@@ -11,6 +11,11 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpdm.so")
+# A/B timing of two builds in one box session (tools/ab_build.sh): PDM_LIB_PATH names another in-tree build;
+# entry points that build lacks are left unbound instead of failing the load
+_AB = os.environ.get("PDM_LIB_PATH")
+if _AB:
+    LIB_PATH = _AB if os.path.isabs(_AB) else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), _AB)
 
 PDM_F32, PDM_BF16, PDM_FP8, PDM_E8M0 = 0, 1, 2, 3
 EPI_BF16, EPI_GELU, EPI_F32, EPI_RES = 0, 1, 2, 3
@@ -115,6 +120,8 @@ _SIGS = {
                                      ctypes.c_void_p]),
     "pdm_attention": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p]),
+    "pdm_attention_log2": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "pdm_f32_to_bf16": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]),
     "pdm_mx_quantize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
@@ -159,6 +166,8 @@ def load():
                            f"g.build()'` (or `make -C panopticdiffusionmodels_amd/csrc`)")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
+        if _AB and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -378,10 +387,15 @@ def layernorm(x, gamma, beta, eps=1e-5):
     return y
 
 
-def attention(qkv, B, L, H, Dh, scale=None):
+def attention(qkv, B, L, H, Dh, scale=None, q_log2=False):
+    """q_log2: q already carries Dh^-0.5 * log2(e) (pdm_attention_log2, the U-ViT forward's layout)."""
     lib = load()
     require_gpu(qkv)
     out = torch.empty(B * L, H * Dh, dtype=torch.bfloat16, device=qkv.device)
+    if q_log2:
+        check(lib.pdm_attention_log2(ptr(qkv), qkv.stride(0), ptr(out), out.stride(0), B, L, H, Dh,
+                                     stream_ptr(qkv.device)), "pdm_attention_log2")
+        return out
     scale = Dh ** -0.5 if scale is None else scale
     check(lib.pdm_attention(ptr(qkv), qkv.stride(0), ptr(out), out.stride(0), B, L, H, Dh, scale,
                             stream_ptr(qkv.device)), "pdm_attention")

@@ -382,6 +382,12 @@ __device__ __forceinline__ i32x4 gload16_asm(const void* ptr) {
   return v;
 }
 
+// q * (scale * log2 e) for kernels whose producer did not pre-scale q (AttentionArgs::q_log2 == 0)
+__device__ __forceinline__ bf16x8 scale_bf16x8(bf16x8 v, float sc) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] * sc);
+  return v;
+}
 // cross-lane max / sum over the four 16-lane rows holding one query's keys (lanes col, col+16, col+32,
 // col+48): v_permlane16/32_swap half exchanges, no LDS round trip (ds_bpermute)
 __device__ __forceinline__ float xrow_max(float v) {
@@ -399,7 +405,9 @@ __device__ __forceinline__ float xrow_sum(float v) {
 
 // NW = waves per workgroup: 4 when two heads fit per CU (L <= 320), else 8 so the single resident head still
 // has two waves per SIMD (t2i image / mask streams, L = 334 / 590)
-template <int DEBUG, int NW>
+// ONES: the softmax row sums come from a fifth PV tile whose V^T operand is a constant ones row (one extra MFMA per
+// 32 keys and tile) instead of VALU adds over the scores
+template <int DEBUG, int NW, bool ONES = false>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(AttentionArgs p, int nqt, int Lp) {
   constexpr int DH = 64;
   constexpr float RESCALE_THR = 8.0f;   // deferred rescale (log2 units): P <= 2^8 in bf16, O / l stay fp32
@@ -477,15 +485,18 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
   // one pass over all keys for NT query tiles (qf), writing the normalised rows of tiles tl[0..NT)
   auto run_pass = [&](auto ntc, const bf16x8 (&qf)[3][2], const int (&tl)[3], bool first) {
     constexpr int NT = decltype(ntc)::value;
+    constexpr int NA = ONES ? 5 : 4;
     float m_run[NT], l_run[NT];
-    f32x4 acc[NT][4];
+    f32x4 acc[NT][NA];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       m_run[t] = -INFINITY;
       l_run[t] = 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < NA; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    const bf16x8 z8 = bf16x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const bf16x8 ones_row = col == 0 ? bf16x8{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f} : z8;   // V^T row 0 of tile 4
     // LDS addresses: both swizzles are independent of the block c and of kt / kk (row = c*64 + kt*16 + col gives
     // (row >> 1) & 7 = (col >> 1) & 7; V row r = c*64 + kk*32 + 4g + qq gives (r >> 1) & 3 = (2g + (qq >> 1)) & 3),
     // so every fragment read is a per-lane base + c * 8 KiB + an immediate offset (no address VALU per read)
@@ -496,14 +507,16 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
       vbase[dt] = Vs + (4 * g + (col >> 2)) * 128 + ((dt ^ ((2 * g + (col >> 3)) & 3)) << 5) + 8 * (col & 3);
-    auto do_block = [&](int c, auto tailc) {
-      constexpr bool TAIL = decltype(tailc)::value;
+    // Scores live in log2 units relative to the running max: Q carries scale * log2(e) (q_log2), and every block
+    // after a pass's first starts its Q K^T accumulators at -m_run, so P = exp2(S) needs no per-score FMA.
+    auto do_block = [&](int c, auto tailc, auto firstc) {
+      constexpr bool TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
       const int kvalid = L - c * 64;
       f32x4 s[NT][4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < NT; ++t) s[t][kt] = FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4(-m_run[t]);
         if (TAIL && kt * 16 >= kvalid) continue;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -528,24 +541,30 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
         for (int kt = 1; kt < 4; ++kt)
 #pragma unroll
           for (int j = 0; j < 4; ++j) m4[j] = fmaxf(m4[j], s[t][kt][j]);
-        const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]))) * sl2;
-        // deferred rescale: keep the running max until a block exceeds it by RESCALE_THR
-        const bool grow = cmax > m_run[t] + RESCALE_THR;
-        const float m_new = grow ? cmax : m_run[t];
-        const float alpha = __builtin_amdgcn_exp2f(m_run[t] - m_new);
-        m_run[t] = m_new;
+        const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
+        if constexpr (FIRST) {   // the running max starts at the first block's
+          m_run[t] = cmax;
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= cmax;
+        } else if (__builtin_amdgcn_ballot_w64(cmax > RESCALE_THR)) {
+          // deferred rescale: the running max moves only when a block exceeds it by RESCALE_THR (rare)
+          const float d = cmax > RESCALE_THR ? cmax : 0.f;
+          const float alpha = __builtin_amdgcn_exp2f(-d);
+          m_run[t] += d;
+          l_run[t] *= alpha;
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= d;
+#pragma unroll
+          for (int i = 0; i < NA; ++i) acc[t][i] *= alpha;
+        }
         f32x4 l4 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(fmaf(s[t][kt][j], sl2, -m_new));
-          l4 += s[t][kt];
+          for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(s[t][kt][j]);
+          if constexpr (!ONES) l4 += s[t][kt];
         }
-        l_run[t] = fmaf(l_run[t], alpha, (l4[0] + l4[1]) + (l4[2] + l4[3]));
-        if (__builtin_amdgcn_ballot_w64(grow)) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[t][i] *= alpha;
-        }
+        if constexpr (!ONES) l_run[t] += (l4[0] + l4[1]) + (l4[2] + l4[3]);
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -567,19 +586,30 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
 #pragma unroll
           for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf, pf[t], acc[t][dt]);
         }
+        if constexpr (ONES) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t][4] = mfma16x16x32(ones_row, pf[t], acc[t][4]);
+        }
       }
     };
-    for (int c = 0; c < nfull; ++c) {
-      if (first) block_ready(c);
-      if (DEBUG != 1) do_block(c, std::false_type{});
+    if (first) block_ready(0);
+    if (DEBUG != 1) {
+      if (nfull > 0) do_block(0, std::false_type{}, std::true_type{});
+      else do_block(0, std::true_type{}, std::true_type{});
     }
-    if (nfull < nch) {
+    for (int c = 1; c < nfull; ++c) {
+      if (first) block_ready(c);
+      if (DEBUG != 1) do_block(c, std::false_type{}, std::false_type{});
+    }
+    if (nfull < nch && nfull > 0) {
       if (first) block_ready(nfull);
-      if (DEBUG != 1) do_block(nfull, std::true_type{});
+      if (DEBUG != 1) do_block(nfull, std::true_type{}, std::false_type{});
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const float inv = 1.0f / xrow_sum(l_run[t]);
+      float lsum = l_run[t];
+      if constexpr (ONES) lsum = g == 0 ? acc[t][NA - 1][0] : 0.f;   // V^T row 0 of tile 4: lanes of k-group 0
+      const float inv = 1.0f / xrow_sum(lsum);
       const int q = tl[t] * 16 + col;
       if (q < L) {
         bf16* orow = p.out + ((size_t)b * L + q) * p.ldo + h * DH;
@@ -622,6 +652,12 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) qf[t][ks] = *reinterpret_cast<const bf16x8*>(qptr(t < nt ? tl[t] : tl[0], ks));
     }
+    if (!p.q_log2) {   // q not pre-scaled by the producer: scale * log2(e) applied here (one extra bf16 rounding)
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) qf[t][ks] = scale_bf16x8(qf[t][ks], sl2);
+    }
     if (nt == 3) run_pass(std::integral_constant<int, 3>{}, qf, tl, pass == 0);
     else if (nt == 2) run_pass(std::integral_constant<int, 2>{}, qf, tl, pass == 0);
     else run_pass(std::integral_constant<int, 1>{}, qf, tl, pass == 0);
@@ -631,9 +667,11 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
 // ------------------------------------------------------------------------------------------------
 // Head-resident kernel for Dh = 72 (U-ViT-H/2 and H/4: libs/uvit.py:66-92 with embed_dim 1152, 16 heads), the
 // v2 structure above with the head dim cut as 64 + 8 instead of padded to 96:
-//   Q K^T: two v_mfma_f32_16x16x32_bf16 k-steps over d 0..63 + one v_mfma_f32_16x16x16_bf16 over d 64..71
-//          (lanes of k-group 2, 3 hold zeros), i.e. 40 instead of 48 MFMA cycles per 16x16 score tile;
-//   P V:   five 16-column output tiles (d 64..79 for the last; rows 72..79 of it are never stored).
+//   Q K^T: three v_mfma_f32_16x16x32_bf16 k-steps, the third over d 64..95 with d 64..71 in k-group 0 and the
+//          running max folded into its padding slot d = 72 (K = 1, Q = -m_run): scores leave the MFMA chain as
+//          q'k - m in log2 units (q carries Dh^-0.5 log2 e), ready for exp2;
+//   P V:   five 16-column output tiles (d 64..79 for the last; rows 73..79 of it are never stored and row 72, with
+//          V^T row 72 := ones, accumulates the softmax row sum).
 // K and V rows stay unpadded (144 B) so a head's K + V fit twice per CU at L = 258:
 //   LDS = [V rows 0 .. round8(L)) [K rows 0 .. round16(L)), 144 B each; staged by LDS-DMA as a flat array of
 //   16-B chunks (chunk ci -> row ci / 9, column chunk ci % 9).  PV reads whole 32-key steps, so V rows past
@@ -654,7 +692,7 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
   const int L = p.L, D = p.H * DH;
   const bf16* base = p.qkv + (size_t)b * L * p.ldq + h * DH;
   const int g = lane >> 4, col = lane & 15;
-  const bool glo = g < 2;   // k-groups holding d 64..71 in the 16x16x16 remainder step
+  const bool glo = g < 2;   // output rows d 64..71 of the fifth PV tile (rows 72..79 are padding)
 
   const int my_tiles = nqt > wave ? (nqt - wave + 3) / 4 : 0;
   const int npass = (my_tiles + 1) / 2;
@@ -666,14 +704,14 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
   };
   // Q fragments of the first pass: d = ks*32 + g*8 .. +7 (x32 steps) and d = 64 + 4g .. +3 (x16 step, g < 2)
   i32x4 q0[2][2];
-  int2 q0r[2];
+  i32x4 q0r[2];   // Q[q][64 .. 71] (used by the lanes of k-group 0)
   if (npass > 0 && DEBUG != 2) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const bf16* qr = qrow(min(wave + 4 * t, nqt - 1));
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) q0[t][ks] = gload16_asm(qr + ks * 32 + g * 8);
-      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(q0r[t]) : "v"(qr + 64 + 4 * (g & 1)) : "memory");
+      q0r[t] = gload16_asm(qr + 64);
     }
   }
   // K / V DMA: 64 chunks (1 KiB) per instruction, instruction i of each tensor issued by wave i % 4, V before K
@@ -705,45 +743,52 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
 
   const float sl2 = p.scale * 1.4426950408889634f;
   const int nfull = L / 64, nch = (L + 63) / 64;
-  const s16x4 zero4 = s16x4{0, 0, 0, 0};
+  const bf16x8 ones8 = bf16x8{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+  const bf16x8 one8 = bf16x8{1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bf16x8 zero8 = bf16x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
-  auto run_pass = [&](auto ntc, const bf16x8 (&qf)[2][2], const s16x4 (&qr)[2], const int (&tl)[2], bool first) {
+  auto run_pass = [&](auto ntc, const bf16x8 (&qf)[2][2], const bf16x8 (&qr)[2], const int (&tl)[2], bool first) {
     constexpr int NT = decltype(ntc)::value;
-    float m_run[NT], l_run[NT];
+    float m_run[NT];
     f32x4 acc[NT][5];
+    bf16x8 qm[NT];   // Q of the d 64..95 step: d 64..71 (k-group 0) and the slot d = 72 (k-group 1) = -m_run
+    auto set_qm = [&](int t) {
+      bf16x8 v = qr[t];
+      if (g == 1) v[0] = (bf16)(-m_run[t]);
+      qm[t] = v;
+    };
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+      qm[t] = qr[t];   // first block: slot 0 (no shift yet)
       m_run[t] = -INFINITY;
-      l_run[t] = 0.f;
 #pragma unroll
       for (int i = 0; i < 5; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     const char* kbase = Ks + col * ROWB;   // per-lane bases; block / kt / kk / dt offsets are immediates
     const char* vbase = Vs + (4 * g + (col >> 2)) * ROWB + 8 * (col & 3);
-    auto do_block = [&](int c, auto tailc) {
-      constexpr bool TAIL = decltype(tailc)::value;
+    // log2-domain scores relative to the running max, as attention_v2_kernel
+    auto do_block = [&](int c, auto tailc, auto firstc) {
+      constexpr bool TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
       const int kvalid = L - c * 64;
       f32x4 s[NT][4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (TAIL && kt * 16 >= kvalid) continue;
         const char* krow = kbase + c * (64 * ROWB) + kt * (16 * ROWB);
+        // a third 16x16x32 step over d 64..95 carries d 64..71 (k-group 0) and, in the padding slot d = 72
+        // (k-group 1), K = 1 against Q = -m_run, so the chain leaves q'k - m_run with no VALU pass over the scores
+        // (one uniform MFMA chain: a 16x16x16 step chained with 16x16x32 ones got too few SrcC wait states
+        // from hipcc on gfx950, measured wrong scores in both orders)
+        bf16x8 kx = *reinterpret_cast<const bf16x8*>(krow + 128);
+        kx = g == 0 ? kx : (g == 1 ? one8 : zero8);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kx, qm[t], f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + (ks * 4 + g) * 16);
 #pragma unroll
           for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kf, qf[t][ks], s[t][kt]);
         }
-        s16x4 kr = *reinterpret_cast<const s16x4*>(krow + 128 + 8 * (g & 1));
-        kr = glo ? kr : zero4;
-        // the d 64..71 step accumulates separately and is added by the VALU: a 16x16x16 MFMA reading as SrcC the
-        // result of the 16x16x32 MFMA just before it got too few wait states from hipcc (ROCm 7.2) on gfx950 when
-        // nothing else was interleaved (NT = 1): wrong scores, measured
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          s[t][kt] += __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kr, qr[t], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       }
       if constexpr (TAIL) {
 #pragma unroll
@@ -761,23 +806,27 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
         for (int kt = 1; kt < 4; ++kt)
 #pragma unroll
           for (int j = 0; j < 4; ++j) m4[j] = fmaxf(m4[j], s[t][kt][j]);
-        const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]))) * sl2;
-        const bool grow = cmax > m_run[t] + RESCALE_THR;
-        const float m_new = grow ? cmax : m_run[t];
-        const float alpha = __builtin_amdgcn_exp2f(m_run[t] - m_new);
-        m_run[t] = m_new;
-        f32x4 l4 = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
+        // m_run stays bf16-representable (it enters the MFMA as a bf16 operand); the shift is exact in fp32
+        if constexpr (FIRST) {
+          m_run[t] = (float)(bf16)cmax;
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt) {
+          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= m_run[t];
+          set_qm(t);
+        } else if (__builtin_amdgcn_ballot_w64(cmax > RESCALE_THR)) {
+          const float d = cmax > RESCALE_THR ? (float)(bf16)(m_run[t] + cmax) - m_run[t] : 0.f;
+          const float alpha = __builtin_amdgcn_exp2f(-d);
+          m_run[t] += d;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(fmaf(s[t][kt][j], sl2, -m_new));
-          l4 += s[t][kt];
-        }
-        l_run[t] = fmaf(l_run[t], alpha, (l4[0] + l4[1]) + (l4[2] + l4[3]));
-        if (__builtin_amdgcn_ballot_w64(grow)) {
+          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= d;
 #pragma unroll
           for (int i = 0; i < 5; ++i) acc[t][i] *= alpha;
+          set_qm(t);
         }
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(s[t][kt][j]);
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -796,23 +845,30 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
         for (int dt = 0; dt < 5; ++dt) {
           const s16x4 lo = lds_read_tr16(v1 + dt * 32);
           const s16x4 hi = lds_read_tr16(v2 + dt * 32);
-          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          // output row d = 72 (padding, never stored) becomes the softmax row sum: V^T row 72 := ones
+          if (dt == 4) vf = (lane & 15) == 8 ? ones8 : vf;
 #pragma unroll
           for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf, pf[t], acc[t][dt]);
         }
       }
     };
-    for (int c = 0; c < nfull; ++c) {
-      if (first) block_ready(c);
-      if (DEBUG != 1) do_block(c, std::false_type{});
+    if (first) block_ready(0);
+    if (DEBUG != 1) {
+      if (nfull > 0) do_block(0, std::false_type{}, std::true_type{});
+      else do_block(0, std::true_type{}, std::true_type{});
     }
-    if (nfull < nch) {
+    for (int c = 1; c < nfull; ++c) {
+      if (first) block_ready(c);
+      if (DEBUG != 1) do_block(c, std::false_type{}, std::false_type{});
+    }
+    if (nfull < nch && nfull > 0) {
       if (first) block_ready(nfull);
-      if (DEBUG != 1) do_block(nfull, std::true_type{});
+      if (DEBUG != 1) do_block(nfull, std::true_type{}, std::false_type{});
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const float inv = 1.0f / xrow_sum(l_run[t]);
+      const float inv = 1.0f / xrow_sum(g == 2 ? acc[t][4][0] : 0.f);   // row d = 72: lanes of k-group 2, j = 0
       const int q = tl[t] * 16 + col;
       if (q < L) {
         bf16* orow = p.out + ((size_t)b * L + q) * p.ldo + h * DH;
@@ -831,7 +887,7 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
     return;
   }
   bf16x8 qf[2][2];
-  s16x4 qr[2];
+  bf16x8 qr[2];
   if (DEBUG != 2) {
     asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]), "+v"(q0r[0]), "+v"(q0r[1]));
   }
@@ -850,7 +906,7 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
       for (int t = 0; t < 2; ++t) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) qf[t][ks] = __builtin_bit_cast(bf16x8, q0[t][ks]);
-        qr[t] = glo ? __builtin_bit_cast(s16x4, q0r[t]) : zero4;
+        qr[t] = g == 0 ? __builtin_bit_cast(bf16x8, q0r[t]) : zero8;
       }
     } else {
 #pragma unroll
@@ -858,8 +914,16 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
         const bf16* r = qrow(t == 0 || two ? tl[t] : tl[0]);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) qf[t][ks] = *reinterpret_cast<const bf16x8*>(r + ks * 32 + g * 8);
-        const s16x4 v = *reinterpret_cast<const s16x4*>(r + 64 + 4 * (g & 1));
-        qr[t] = glo ? v : zero4;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(r + 64);
+        qr[t] = g == 0 ? v : zero8;
+      }
+    }
+    if (!p.q_log2) {   // q not pre-scaled by the producer: scale * log2(e) applied here (one extra bf16 rounding)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) qf[t][ks] = scale_bf16x8(qf[t][ks], sl2);
+        qr[t] = scale_bf16x8(qr[t], sl2);
       }
     }
     if (two) run_pass(std::integral_constant<int, 2>{}, qf, qr, tl, pass == 0);
@@ -881,7 +945,8 @@ const char* attention_check(const AttentionArgs& p) {
 static int g_attention_algo = 0;   // 0 auto, 1 streamed K/V, 2/3 head-resident T = 2/3, 4 head-resident v2 (5/6 timing)
 void attention_set_algo(int algo) { g_attention_algo = algo; }
 
-hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream) {
+hipError_t attention_launch(const AttentionArgs& args, hipStream_t stream) {
+  AttentionArgs p = args;
   const int nqt = (p.L + 15) / 16;
   int algo = g_attention_algo;
   const int Lp = (p.L + 31) / 32 * 32;   // PV reads whole 32-key steps
@@ -907,30 +972,45 @@ hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream) {
   // automatic: the head-resident v2 structure wherever the head's K/V fit in LDS (Dh = 64: every U-ViT-S/M/L
   // shape); measured 152 vs 213 us (streamed) on L/2 at 190 rows (tools/attn_bench.py)
   if (algo == 0 && p.Dh == 64 && Lp * 256 <= 160 * 1024) algo = 4;
+  if (algo == 10 && p.Dh == 64 && Lp * 256 <= 160 * 1024) {   // v2 with VALU row sums (A/B: 145.7 vs 140.1 us, L/2)
+    const int smem = Lp * 256;
+    static bool attr10 = false;
+    if (!attr10) {
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0, 4, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0, 8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr10 = true;
+    }
+    if (smem <= 80 * 1024) hipLaunchKernelGGL((attention_v2_kernel<0, 4, false>), dim3(p.B * p.H), dim3(256), smem, stream, p, nqt, Lp);
+    else hipLaunchKernelGGL((attention_v2_kernel<0, 8, false>), dim3(p.B * p.H), dim3(512), smem, stream, p, nqt, Lp);
+    return hipGetLastError();
+  }
   if (algo >= 4 && algo <= 6 && p.Dh == 64 && Lp * 256 <= 160 * 1024) {
     const int smem = Lp * 256;
     static bool attr2 = false;
     if (!attr2) {
-      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipFuncSetAttribute((const void*)attention_v2_kernel<1, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipFuncSetAttribute((const void*)attention_v2_kernel<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_v2_kernel<0, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipFuncSetAttribute((const void*)attention_v2_kernel<1, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipFuncSetAttribute((const void*)attention_v2_kernel<2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr2 = true;
     }
     const dim3 grid(p.B * p.H);
     if (smem <= 80 * 1024) {   // two heads per CU: 4 waves each
-      if (algo == 4) hipLaunchKernelGGL((attention_v2_kernel<0, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
+      if (algo == 4) hipLaunchKernelGGL((attention_v2_kernel<0, 4, true>), grid, dim3(256), smem, stream, p, nqt, Lp);
       else if (algo == 5) hipLaunchKernelGGL((attention_v2_kernel<1, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
       else hipLaunchKernelGGL((attention_v2_kernel<2, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
     } else {                   // one head per CU: 8 waves (two per SIMD)
-      if (algo == 4) hipLaunchKernelGGL((attention_v2_kernel<0, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
+      if (algo == 4) hipLaunchKernelGGL((attention_v2_kernel<0, 8, true>), grid, dim3(512), smem, stream, p, nqt, Lp);
       else if (algo == 5) hipLaunchKernelGGL((attention_v2_kernel<1, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
       else hipLaunchKernelGGL((attention_v2_kernel<2, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
     }
     return hipGetLastError();
   }
+  // the kernels below compute exp2(S * scale * log2 e): with q pre-scaled by scale * log2(e) (q_log2) they take
+  // scale = ln 2 (the head-resident kernels above read q_log2 themselves and work in log2 units either way)
+  if (p.q_log2) p.scale = 0.69314718055994531f;
   if (algo == 0 || algo >= 4) algo = 1;
   if (algo == 2 || algo == 3) {
     const int T = algo;

@@ -322,6 +322,7 @@ int run_block(const Ctx& c, const std::string& pre, float* X, int nseq, int L, c
     a.out = w.ATT; a.ldo = D;
     a.B = nseq; a.L = L; a.H = h->H; a.Dh = h->Dh;
     a.scale = 1.0f / sqrtf((float)h->Dh);
+    a.q_log2 = 1;   // attn.qkv's q rows are packed pre-scaled by Dh^-0.5 log2(e) (include/pdm.h)
     PDM_CHECK(pdm::attention_check(a));
     PDM_HIP(pdm::attention_launch(a, c.s));
   }
@@ -393,6 +394,7 @@ int run_block16(const Ctx& c, const std::string& pre, int nseq, int L, const bf1
     a.out = w.ATT; a.ldo = D;
     a.B = nseq; a.L = L; a.H = h->H; a.Dh = h->Dh;
     a.scale = 1.0f / sqrtf((float)h->Dh);
+    a.q_log2 = 1;   // attn.qkv's q rows are packed pre-scaled by Dh^-0.5 log2(e) (include/pdm.h)
     PDM_CHECK(pdm::attention_check(a));
     PDM_HIP(pdm::attention_launch(a, c.s));
   }
@@ -506,6 +508,7 @@ int run_block8(const Ctx& c, const std::string& pre, float* X, int M, int L, con
     at.out = w.ATT; at.ldo = D;
     at.B = M / L; at.L = L; at.H = h->H; at.Dh = h->Dh;
     at.scale = 1.0f / sqrtf((float)h->Dh);
+    at.q_log2 = 1;
     PDM_CHECK(pdm::attention_check(at));
     PDM_HIP(pdm::attention_launch(at, c.s));
     PDM_HIP(pdm::mxq_launch(w.ATT, 1, D, M, D, w.atq.q, w.atq.ld, w.atq.s, w.atq.sld, c.s));
@@ -740,8 +743,8 @@ int pdm_set_gemm_tuning(int raster, int dbg_tile0) {
 }
 
 int pdm_set_attention_algo(int algo) {
-  if (algo < 0 || algo > 9)
-    return fail(PDM_ERR_ARG, "pdm_set_attention_algo: algo must be 0 (auto) or 1..9 (5, 6, 8, 9: timing experiments)");
+  if (algo < 0 || algo > 10)
+    return fail(PDM_ERR_ARG, "pdm_set_attention_algo: algo must be 0 (auto) or 1..10 (5, 6, 8, 9: timing experiments)");
   pdm::attention_set_algo(algo);
   return PDM_OK;
 }
@@ -1192,6 +1195,15 @@ int pdm_attention(const void* qkv, int ldq, void* out, int ldo, int B, int L, in
   pdm::AttentionArgs a{};
   a.qkv = (const bf16*)qkv; a.ldq = ldq; a.out = (bf16*)out; a.ldo = ldo;
   a.B = B; a.L = L; a.H = H; a.Dh = Dh; a.scale = scale;
+  PDM_CHECK(pdm::attention_check(a));
+  PDM_HIP(pdm::attention_launch(a, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_attention_log2(const void* qkv, int ldq, void* out, int ldo, int B, int L, int H, int Dh, void* stream) {
+  pdm::AttentionArgs a{};
+  a.qkv = (const bf16*)qkv; a.ldq = ldq; a.out = (bf16*)out; a.ldo = ldo;
+  a.B = B; a.L = L; a.H = H; a.Dh = Dh; a.scale = 1.0f / sqrtf((float)Dh); a.q_log2 = 1;
   PDM_CHECK(pdm::attention_check(a));
   PDM_HIP(pdm::attention_launch(a, (hipStream_t)stream));
   return PDM_OK;

@@ -116,6 +116,7 @@ struct AttentionArgs {
   bf16* out; int ldo;
   int B, L, H, Dh;
   float scale;
+  int q_log2;                 // q already multiplied by scale * log2(e) (the U-ViT qkv weights are packed so)
 };
 const char* attention_check(const AttentionArgs& p);
 hipError_t attention_launch(const AttentionArgs& p, hipStream_t stream);

@@ -40,38 +40,42 @@ def interpolate_fn(x, xp, yp):
 
 
 class NoiseScheduleVP:
+    """dpm_solver_pp.py:55-169 API as tensor functions over ONE schedule object: the float64 host schedule
+    (solver_core.HostDiscrete / HostLinear / HostCosine) that the fused samplers' coefficients come from.  The
+    discrete knots are that object's (built in fp32 exactly like the reference), the linear / cosine constants
+    its attributes, so the tensor API and the samplers cannot drift apart."""
+
     def __init__(self, schedule='discrete', beta_0=1e-4, beta_1=2e-2, total_N=1000, betas=None, alphas_cumprod=None):
         """dpm_solver_pp.py:56-119."""
         if schedule not in ['linear', 'discrete', 'cosine']:
             raise ValueError("Unsupported noise schedule {}. The schedule needs to be 'linear' or 'cosine'".format(schedule))
+        self.schedule = schedule
         self.total_N = total_N
         self.beta_0 = beta_0 * 1000.
         self.beta_1 = beta_1 * 1000.
         if schedule == 'discrete':
             if betas is not None:
-                log_alphas = 0.5 * torch.log(1 - torch.as_tensor(betas).float()).cumsum(dim=0)
                 self._host = sc.HostDiscrete(betas=betas)
             else:
                 assert alphas_cumprod is not None
-                log_alphas = 0.5 * torch.log(torch.as_tensor(alphas_cumprod).float())
                 self._host = sc.HostDiscrete(alphas_cumprod=alphas_cumprod)
-            self.total_N = len(log_alphas)
-            self.t_discrete = torch.linspace(1. / self.total_N, 1., self.total_N).reshape((1, -1))
-            self.log_alpha_discrete = log_alphas.reshape((1, -1)).cpu()
+            self.total_N = self._host.N
+            self.t_discrete = torch.from_numpy(self._host.t_knots).float().reshape((1, -1))
+            self.log_alpha_discrete = torch.from_numpy(self._host.log_alpha).float().reshape((1, -1))
         elif schedule == 'linear':
             self._host = sc.HostLinear(self.beta_0, self.beta_1)
         else:
             self._host = sc.HostCosine()
-        self.cosine_s = 0.008
+        cos = self._host if schedule == 'cosine' else sc.HostCosine()
+        self.cosine_s = cos.s
         self.cosine_beta_max = 999.
         self.cosine_t_max = math.atan(self.cosine_beta_max * (1. + self.cosine_s) / math.pi) * 2. * (1. + self.cosine_s) / math.pi - self.cosine_s
-        self.cosine_log_alpha_0 = math.log(math.cos(self.cosine_s / (1. + self.cosine_s) * math.pi / 2.))
-        self.schedule = schedule
-        self.T = 0.9946 if schedule == 'cosine' else 1.
+        self.cosine_log_alpha_0 = cos.la0
+        self.T = self._host.T
 
     def marginal_log_mean_coeff(self, t):
         if self.schedule == 'linear':
-            return -0.25 * t ** 2 * (self.beta_1 - self.beta_0) - 0.5 * t * self.beta_0
+            return -0.25 * t ** 2 * (self._host.b1 - self._host.b0) - 0.5 * t * self._host.b0
         if self.schedule == 'discrete':
             return interpolate_fn(t.reshape((-1, 1)), self.t_discrete.to(t.device),
                                   self.log_alpha_discrete.to(t.device)).reshape((-1,))
@@ -91,9 +95,10 @@ class NoiseScheduleVP:
 
     def inverse_lambda(self, lamb):
         if self.schedule == 'linear':
-            tmp = 2. * (self.beta_1 - self.beta_0) * torch.logaddexp(-2. * lamb, torch.zeros((1,)).to(lamb))
-            Delta = self.beta_0 ** 2 + tmp
-            return tmp / (torch.sqrt(Delta) + self.beta_0) / (self.beta_1 - self.beta_0)
+            b0, b1 = self._host.b0, self._host.b1
+            tmp = 2. * (b1 - b0) * torch.logaddexp(-2. * lamb, torch.zeros((1,)).to(lamb))
+            Delta = b0 ** 2 + tmp
+            return tmp / (torch.sqrt(Delta) + b0) / (b1 - b0)
         if self.schedule == 'discrete':
             log_alpha = -0.5 * torch.logaddexp(torch.zeros((1,)).to(lamb.device), -2. * lamb)
             t = interpolate_fn(log_alpha.reshape((-1, 1)), torch.flip(self.log_alpha_discrete.to(lamb.device), [1]),

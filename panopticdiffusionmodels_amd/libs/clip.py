@@ -142,12 +142,19 @@ class CLIPTextEncoder(nn.Module):
         self.encoder = _Encoder(hidden_size, intermediate_size, num_hidden_layers)
         self.final_layer_norm = nn.LayerNorm(hidden_size, eps=layer_norm_eps)
         self._native = None
+        # encoding with the constructor's default init is refused unless weights were loaded or the caller opted
+        # into synthetic weights (benchmarks): a ported sample script must not silently run an untrained encoder
+        self.weights_loaded = False
+        self.allow_synthetic_weights = False
 
     def _apply(self, fn, *args, **kwargs):
         self._native = None
         return super()._apply(fn, *args, **kwargs)
 
     def load_state_dict(self, state_dict, strict=True, *args, **kwargs):
+        """Accepts CLIPTextModel keys with or without the `text_model.` / reference `transformer.text_model.`
+        prefix; position_ids buffers are dropped.  strict=True (the default) fails on any missing or unexpected
+        key."""
         self._native = None
         sd = {}
         for k, v in state_dict.items():
@@ -158,10 +165,15 @@ class CLIPTextEncoder(nn.Module):
             if k.endswith("position_ids"):   # buffer of older transformers checkpoints
                 continue
             sd[k] = v
-        return super().load_state_dict(sd, strict, *args, **kwargs)
+        res = super().load_state_dict(sd, strict, *args, **kwargs)
+        self.weights_loaded = True
+        return res
 
     @torch.no_grad()
     def forward(self, input_ids):
+        if not (self.weights_loaded or self.allow_synthetic_weights):
+            raise RuntimeError("CLIP text encoder: no weights loaded (FrozenCLIPEmbedder(version=<local checkpoint "
+                               "dir>) or load_state_dict); pass synthetic=True to encode with the default init")
         dev = self.final_layer_norm.weight.device
         _lib.require_gpu(self.final_layer_norm.weight)
         ids = torch.as_tensor(input_ids).to(device=dev, dtype=torch.int64)
@@ -186,11 +198,14 @@ class CLIPTextEncoder(nn.Module):
 
 class FrozenCLIPEmbedder(nn.Module):
     """libs/clip.py:13-38.  `version` is a LOCAL directory holding the CLIP checkpoint (config.json +
-    pytorch_model.bin / model.safetensors) and tokenizer files, or None for the ViT-L/14 text shape with
-    weights loaded later through load_state_dict; `tokenizer` overrides the tokenizer (a callable with the
-    transformers CLIPTokenizer call signature, or None when only `encode_tokens` is used)."""
+    pytorch_model.bin / model.safetensors) and tokenizer files (loaded strictly: every text-tower key must be
+    present), or None for the ViT-L/14 text shape with weights loaded later through
+    `transformer.load_state_dict` -- encoding before that raises unless synthetic=True (benchmarks on seeded
+    weights).  `tokenizer` overrides the tokenizer (a callable with the transformers CLIPTokenizer call
+    signature, or None when only `encode_tokens` is used).  Unlike the reference's no-argument constructor,
+    nothing is downloaded: there is no implicit openai/clip-vit-large-patch14."""
 
-    def __init__(self, version=None, device="cuda", max_length=77, tokenizer=None, config=None):
+    def __init__(self, version=None, device="cuda", max_length=77, tokenizer=None, config=None, synthetic=False):
         super().__init__()
         cfg = dict(VIT_L14_TEXT)
         self.tokenizer = tokenizer
@@ -208,8 +223,9 @@ class FrozenCLIPEmbedder(nn.Module):
         if config is not None:
             cfg.update(config)
         self.transformer = CLIPTextEncoder(**cfg)
+        self.transformer.allow_synthetic_weights = bool(synthetic)
         if version is not None:
-            self.transformer.load_state_dict(_load_local_weights(version), strict=False)
+            self.transformer.load_state_dict(_load_local_weights(version), strict=True)
         self.device = device
         self.max_length = max_length
         self.freeze()

@@ -8,6 +8,7 @@ multiple of 16 rows; conv / embedding tables fp32; norm1 / norm2 folded into att
 registered with the handle.  Any load_state_dict / .to() invalidates the packed copy.
 """
 import ctypes
+import math
 
 import torch
 import torch.nn as nn
@@ -88,11 +89,12 @@ class NativeHandle:
         _lib.check(lib.pdm_uvit_validate(h), "pdm_uvit_validate")
         self._mx = {}
 
-    @staticmethod
-    def _ln_fold(sd, name, fp32=False):
+    def _ln_fold(self, sd, name, fp32=False):
         """norm1 -> attn.qkv and norm2 -> mlp.fc1 are fused (libs/uvit.py:115-120): LN(x) W^T + b =
-        rstd * (x (W diag(g))^T - mean * colsum) + (W beta + b).  Returns the packed tensor for the folded
-        weight / its row sums / the folded bias, or None when `name` is not one of them."""
+        rstd * (x (W diag(g))^T - mean * colsum) + (W beta + b).  attn.qkv's q rows (the first embed_dim) also
+        carry the softmax scale in base 2, Dh^-0.5 log2(e) (libs/uvit.py:64,73), so the attention kernels take
+        exp2 of the scores directly (include/pdm.h).  Returns the packed tensor for the folded weight / its row
+        sums / the folded bias, or None when `name` is not one of them."""
         for lin, norm in ((".attn.qkv", ".norm1"), (".mlp.fc1", ".norm2")):
             for part in (".weight", ".ln_colsum", ".ln_bias"):
                 if not name.endswith(lin + part):
@@ -100,6 +102,12 @@ class NativeHandle:
                 pre = name[: -len(lin + part)]
                 w = sd[pre + lin + ".weight"].detach().float()
                 g = sd[pre + norm + ".weight"].detach().float()
+                rs = None
+                if lin == ".attn.qkv":
+                    D, H = int(self.cfg.embed_dim), int(self.cfg.num_heads)
+                    rs = torch.ones(w.shape[0], dtype=torch.float64, device=w.device)
+                    rs[:D] = (D // H) ** -0.5 * math.log2(math.e)
+                    w = (w.double() * rs[:, None]).float()
                 if part == ".weight" and fp32:
                     return w * g[None, :]
                 wg = (w * g[None, :]).to(torch.bfloat16)
@@ -109,7 +117,8 @@ class NativeHandle:
                     return wg.double().sum(1).float()
                 b = (w.double() @ sd[pre + norm + ".bias"].detach().double())
                 if pre + lin + ".bias" in sd:
-                    b = b + sd[pre + lin + ".bias"].detach().double()
+                    lb = sd[pre + lin + ".bias"].detach().double()
+                    b = b + (lb * rs if rs is not None else lb)
                 return b.float()
         return None
 
@@ -143,7 +152,7 @@ class NativeHandle:
                 if t.numel() != numel:
                     raise RuntimeError(f"parameter {name!r}: {t.numel()} elements, the HIP layout expects {numel}")
                 return t.contiguous()
-        folded = NativeHandle._ln_fold(sd, name)
+        folded = self._ln_fold(sd, name)
         if folded is not None:
             t = folded.to(device=dev, dtype=torch.bfloat16 if dtype == _lib.PDM_BF16 else torch.float32)
             t = t.contiguous().reshape(-1)

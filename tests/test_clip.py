@@ -97,6 +97,24 @@ def test_embedder_without_tokenizer_raises():
         FrozenCLIPEmbedder(version="openai/clip-vit-large-patch14")
 
 
+def test_embedder_refuses_unloaded_weights(tmp_path):
+    """The default-initialised encoder is not silently used; a local checkpoint loads strictly."""
+    from panopticdiffusionmodels_amd.libs.clip import FrozenCLIPEmbedder
+    cfg = dict(vocab_size=64, hidden_size=64, intermediate_size=128, num_hidden_layers=1, num_attention_heads=2)
+    e = FrozenCLIPEmbedder(config=cfg)
+    with pytest.raises(RuntimeError, match="no weights loaded"):
+        e.encode_tokens(torch.zeros(1, 4, dtype=torch.int64))
+    # a checkpoint directory with a key missing fails at construction (strict loading)
+    import json
+    from safetensors.torch import save_file
+    sd = {"text_model." + k: v.contiguous() for k, v in e.transformer.state_dict().items()}
+    sd.pop("text_model.final_layer_norm.bias")
+    (tmp_path / "config.json").write_text(json.dumps(cfg))
+    save_file(sd, str(tmp_path / "model.safetensors"))
+    with pytest.raises(RuntimeError, match="final_layer_norm.bias"):
+        FrozenCLIPEmbedder(version=str(tmp_path), tokenizer=lambda *a, **k: None, config=cfg)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["clip_dh32", "clip_dh64"])
 def test_hip_clip_vs_transformers_golden(cg, name):
@@ -114,7 +132,7 @@ def test_hip_clip_vs_transformers_golden(cg, name):
 def test_hip_clip_full_vit_l14_vs_oracle():
     from panopticdiffusionmodels_amd.libs.clip import FrozenCLIPEmbedder
     torch.manual_seed(0)
-    e = FrozenCLIPEmbedder()   # ViT-L/14 text shape, random weights (no checkpoint offline)
+    e = FrozenCLIPEmbedder(synthetic=True)   # ViT-L/14 text shape, random weights (no checkpoint offline)
     sd = e.transformer.state_dict()
     with torch.no_grad():
         for k, v in sd.items():

@@ -254,13 +254,21 @@ def test_layernorm(lib, rows, D):
 
 @pytest.mark.parametrize("L", [66, 257, 258, 334, 590])
 @pytest.mark.parametrize("Dh", [32, 64, 72])
-def test_attention(lib, L, Dh):
+@pytest.mark.parametrize("q_log2", [False, True])
+def test_attention(lib, L, Dh, q_log2):
+    """q_log2: q pre-scaled by Dh^-0.5 log2(e) as the U-ViT forward's qkv GEMM writes it (pdm_attention_log2)."""
     H, B = 3, 2
     D = H * Dh
     g = torch.Generator(device="cuda").manual_seed(L * 10 + Dh)
     qkv = (torch.randn(B * L, 3 * D, device="cuda", generator=g) * 1.5).bfloat16()
-    out = lib.attention(qkv, B, L, H, Dh)
     q, k, v = qkv.float().reshape(B, L, 3, H, Dh).permute(2, 0, 3, 1, 4)
+    if q_log2:
+        sq = qkv.clone()
+        sq[:, :D] = (qkv[:, :D].float() * (Dh ** -0.5 * 1.4426950408889634)).bfloat16()
+        out = lib.attention(sq, B, L, H, Dh, q_log2=True)
+        q = sq[:, :D].float().reshape(B, L, H, Dh).permute(0, 2, 1, 3) / (Dh ** -0.5 * 1.4426950408889634)
+    else:
+        out = lib.attention(qkv, B, L, H, Dh)
     ref = torch.softmax(q @ k.transpose(-1, -2) * Dh ** -0.5, dim=-1) @ v
     ref = ref.permute(0, 2, 1, 3).reshape(B * L, D)
     assert rel(out.float(), ref) < 1e-2

@@ -1,5 +1,6 @@
 """A/B timing of the attention structures on one U-ViT shape (dev tool, one process, interleaved rounds).
-python tools/attn_bench.py [rows L H Dh]"""
+python tools/attn_bench.py [rows L H Dh [algos [q_log2 0|1]]]  (q_log2 1, the default: q pre-scaled as the
+U-ViT forward's qkv GEMM writes it, pdm_attention_log2)"""
 import sys
 
 import torch
@@ -13,10 +14,11 @@ g = torch.Generator(device="cuda").manual_seed(0)
 qkv = torch.randn(rows * L, 3 * H * Dh, device="cuda", generator=g).bfloat16()
 flops = 4.0 * rows * H * L * L * Dh
 algos = [int(a) for a in sys.argv[5].split(',')] if len(sys.argv) > 5 else [1, 2, 3, 4, 5, 6]
+LOG2 = bool(int(sys.argv[6])) if len(sys.argv) > 6 else True
 outs = {}
 for a in algos:
     assert lib.pdm_set_attention_algo(a) == 0, lib.pdm_last_error()
-    outs[a] = _lib.attention(qkv, rows, L, H, Dh).float()
+    outs[a] = _lib.attention(qkv, rows, L, H, Dh, q_log2=LOG2).float()
 err = max([float((outs[algos[0]] - outs[a]).norm() / outs[algos[0]].norm()) for a in algos if a not in (5, 6, 8, 9)] + [0.0])
 times = {a: [] for a in algos}
 for rnd in range(7):
@@ -25,7 +27,7 @@ for rnd in range(7):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(10):
-            _lib.attention(qkv, rows, L, H, Dh)
+            _lib.attention(qkv, rows, L, H, Dh, q_log2=LOG2)
         e1.record()
         torch.cuda.synchronize()
         times[a].append(e0.elapsed_time(e1) / 10)

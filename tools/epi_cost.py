@@ -58,6 +58,11 @@ for name, N, K, kind in shapes:
         variants["f32_acc"] = lambda: _lib.gemm_ex(_lib.EPI_F32, a, W, bias, out_f32=X, accumulate=True)
         variants["f32_acc_b_st"] = lambda: _lib.gemm_ex(_lib.EPI_F32, a, W, bias, out_f32=X, accumulate=True, out=Xb,
                                                         stats_out=st_out)
+        # the bf16 residual stream (EPI_RES): write only / read + write / + LayerNorm partials (the forward's form)
+        variants["res"] = lambda: _lib.gemm_ex(_lib.EPI_RES, a, W, bias, out=Xb)
+        variants["res_acc"] = lambda: _lib.gemm_ex(_lib.EPI_RES, a, W, bias, out=Xb, res_in=Xb, accumulate=True)
+        variants["res_acc_st"] = lambda: _lib.gemm_ex(_lib.EPI_RES, a, W, bias, out=Xb, res_in=Xb, accumulate=True,
+                                                      stats_out=st_out)
     def tuned(dbg, fn):
         def run():
             lib.pdm_set_gemm_tuning(0, dbg)
