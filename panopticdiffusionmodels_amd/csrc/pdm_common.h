@@ -23,52 +23,46 @@ __device__ __forceinline__ void glds16(const void* gptr, PDM_LDS void* lds_wave_
   __builtin_amdgcn_global_load_lds(gptr, lds_wave_base, 16, 0, 0);
 }
 
-// nn.GELU() default, exact erf form (libs/uvit.py:98 / libs/timm.py:102), with erf from Abramowitz & Stegun
-// 7.1.28: erf(z) = 1 - p(z)^-16, p a degree-6 polynomial, |err| <= 3e-7 for z >= 0 -- far below the bf16
-// rounding (3.9e-3) of the GEMM outputs it feeds.  One reciprocal (no exp), odd symmetry folded in without
-// cancellation:  GELU(x) = max(x, 0) - 0.5 |x| p(|x| / sqrt 2)^-16  (|abs err| <= 5e-7 over the real line)
+// nn.GELU() default, exact erf form (libs/uvit.py:98 / libs/timm.py:102):  GELU(x) = x Phi(x) = x (1/2 + x P(x^2)).
+// Phi - 1/2 is odd, so it is fitted as  s Q(s^2 - 1/2),  s = clamp(x / 4.5, -1, 1),  Q of degree 9: a minimax fit
+// (linear programme over [0, 4.5]) constrained to Phi(4.5) := 1 exactly, so GELU(x) is exactly 0 for x <= -4.5
+// and exactly x for x >= 4.5 (the true tails differ by < 1.6e-5).  The centred variable s^2 - 1/2 keeps the
+// coefficients O(1) (no fp32 cancellation in Horner); the constant term is nudged so that fp32 Q(1/2) = 1/2.
+// Error over the real line: |abs| <= 1.8e-5, relative <= 9.5e-4 wherever |GELU| > 1e-2 -- under half a bf16 ulp of
+// the GEMM outputs it feeds.  No transcendental: 13 FMA/multiplies and 2 clamps, all packable two-wide.
+#define PDM_GELU_COEFFS                                                                                        \
+  7.060773373e-01f, -6.946521401e-01f, 9.834588766e-01f, -1.449834466e+00f, 2.078067064e+00f,                  \
+      -2.640194416e+00f, 2.778215170e+00f, -3.625102520e+00f, 5.720444202e+00f, -4.195198536e+00f
 __device__ __forceinline__ float gelu_erf(float x) {
-  const float a = fabsf(x);
-  const float z = a * 0.70710678118654752440f;
-  float p = fmaf(z, 4.30638e-5f, 2.765672e-4f);
-  p = fmaf(p, z, 1.520143e-4f);
-  p = fmaf(p, z, 9.2705272e-3f);
-  p = fmaf(p, z, 4.22820123e-2f);
-  p = fmaf(p, z, 7.05230784e-2f);
-  p = fmaf(p, z, 1.0f);
-  float r = __builtin_amdgcn_rcpf(p);
-  r *= r;
-  r *= r;
-  r *= r;
-  r *= r;
-  return fmaf(-0.5f * a, r, fmaxf(x, 0.0f));
+  constexpr float c[10] = {PDM_GELU_COEFFS};
+  const float s = __builtin_amdgcn_fmed3f(x * (1.0f / 4.5f), -1.0f, 1.0f);
+  const float v = fmaf(s, s, -0.5f);
+  float p = c[9];
+#pragma unroll
+  for (int k = 8; k >= 0; --k) p = fmaf(p, v, c[k]);
+  return x * fmaf(s, p, 0.5f);
 }
 
-// The same GELU on two values at once, written on 2-wide vectors so the polynomial, the squarings and the final
-// FMA issue as packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes' work per VALU cycle); only the
-// reciprocals stay scalar.  max(x, 0) is folded as (x + |x|) / 2 (exact), so the tail is
-// GELU = 0.5 (x + |x| - |x| p^-16): one packed add, FMA and multiply, no scalar max / NaN canonicalisation
-// (within 1 ulp of gelu_erf).
+// The same GELU on two values at once, written on 2-wide vectors so the scaling, the polynomial and the final
+// multiply issue as packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes' work per VALU cycle); only the two
+// clamps stay scalar.  Bit-identical to gelu_erf.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
-  const f32x2 a = __builtin_elementwise_abs(x);
-  const f32x2 z = a * 0.70710678118654752440f;
-  f32x2 p = __builtin_elementwise_fma(z, f32x2(4.30638e-5f), f32x2(2.765672e-4f));
-  p = __builtin_elementwise_fma(p, z, f32x2(1.520143e-4f));
-  p = __builtin_elementwise_fma(p, z, f32x2(9.2705272e-3f));
-  p = __builtin_elementwise_fma(p, z, f32x2(4.22820123e-2f));
-  p = __builtin_elementwise_fma(p, z, f32x2(7.05230784e-2f));
-  p = __builtin_elementwise_fma(p, z, f32x2(1.0f));
-  f32x2 r = {__builtin_amdgcn_rcpf(p[0]), __builtin_amdgcn_rcpf(p[1])};
-  r *= r;
-  r *= r;
-  r *= r;
-  r *= r;
-  return __builtin_elementwise_fma(-a, r, x + a) * 0.5f;
+  constexpr float c[10] = {PDM_GELU_COEFFS};
+  f32x2 s = x * (1.0f / 4.5f);
+  s[0] = __builtin_amdgcn_fmed3f(s[0], -1.0f, 1.0f);
+  s[1] = __builtin_amdgcn_fmed3f(s[1], -1.0f, 1.0f);
+  const f32x2 v = __builtin_elementwise_fma(s, s, f32x2(-0.5f));
+  f32x2 p = f32x2(c[9]);
+#pragma unroll
+  for (int k = 8; k >= 0; --k) p = __builtin_elementwise_fma(p, v, f32x2(c[k]));
+  return x * __builtin_elementwise_fma(s, p, f32x2(0.5f));
 }
+#undef PDM_GELU_COEFFS
 
 // quick GELU (transformers QuickGELUActivation, CLIP text encoder): x * sigmoid(1.702 x)
-__device__ __forceinline__ float gelu_quick(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+// (hardware reciprocal instead of the IEEE divide: 1 ulp, and exp overflow for x << 0 still gives -0)
+__device__ __forceinline__ float gelu_quick(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x)); }
 __device__ __forceinline__ float gelu_act(int act, float x) { return act ? gelu_quick(x) : gelu_erf(x); }
 
 __device__ __forceinline__ float wave_sum(float v) {

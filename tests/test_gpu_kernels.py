@@ -47,6 +47,32 @@ def test_gemm(lib, M, N, K, epi):
         assert rel(out, ref + r0) < 2e-3
 
 
+@pytest.mark.parametrize("algo", [0, 1, 7])
+def test_gelu_activation_exactness(lib, algo):
+    """The GELU epilogue alone: A's column 0 carries x, W = e_0, so C = x exactly in fp32 and the output is the
+    bf16 rounding of the kernel's GELU(x).  Against exact-erf GELU in fp64: within one bf16 ulp everywhere
+    or 2e-5 absolute where GELU ~ 0 (the polynomial's own error is <= 1.8e-5 abs / 9.5e-4 rel,
+    csrc/pdm_common.h), exact 0 / x in the tails."""
+    M, N, K = 4096, 256, 64
+    xs = torch.linspace(-8.0, 8.0, M, device="cuda").bfloat16()
+    a = torch.zeros(M, K, device="cuda", dtype=torch.bfloat16)
+    a[:, 0] = xs
+    w = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
+    w[:, 0] = 1
+    lib.load().pdm_set_gemm_algo(algo)
+    try:
+        out = lib.gemm(a, w, None, lib.EPI_GELU).double()
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+    x = xs.double()
+    ref = (x * 0.5 * (1 + torch.erf(x / 2 ** 0.5)))[:, None].expand(M, N)
+    ulp = torch.exp2(torch.floor(torch.log2(ref.abs().clamp_min(2.0 ** -126))) - 7)
+    assert float(((out - ref).abs() / ulp.clamp_min(2e-5)).max()) <= 1.0   # 2e-5 abs where GELU ~ 0
+    assert float(out[x[:, None].expand(M, N) <= -4.5].abs().max()) == 0.0
+    big = x[:, None].expand(M, N) >= 4.5
+    assert torch.equal(out[big], x[:, None].expand(M, N)[big])
+
+
 def test_gemm_split_k(lib):
     g = torch.Generator(device="cuda").manual_seed(1)
     M, D = 517, 256

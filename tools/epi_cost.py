@@ -73,6 +73,8 @@ for name, N, K, kind in shapes:
         return run
     variants["nostore"] = tuned(2, lambda: _lib.gemm_ex(_lib.EPI_BF16, a, W, bias))
     variants["halfstore"] = tuned(4, lambda: _lib.gemm_ex(_lib.EPI_BF16, a, W, bias, out=o))
+    # every row tile stores onto rows 0..255 (an L2-resident 256 x N output): the store cost without HBM write-back
+    variants["l2store"] = tuned(8, lambda: _lib.gemm_ex(_lib.EPI_BF16, a, W, bias, out=o))
     variants["hipblaslt"] = lambda: torch.nn.functional.linear(a, W)
     line = f"{name:5s} M={M} N={N} K={K}"
     for k, fn in variants.items():
