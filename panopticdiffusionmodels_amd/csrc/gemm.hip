@@ -853,8 +853,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)n, 0x00020000);
 }
 
-template <int EPI, int CONV, int SCHED>
+// HN (half-N, N <= 128, SCHED 2 only): a 256 x 128 tile -- the W1 half is never loaded and only the qj = 0
+// quadrants are computed (the decoder's 128-channel 512^2 convs would otherwise waste half of every 256 x 256
+// tile or run on the 128-tile kernel); the epilogue is the 256-wide one, columns >= N are never stored.
+template <int EPI, int CONV, int SCHED, int HN = 0>
 __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n, int nwg) {
+  static_assert(!HN || SCHED == 2, "the half-N tile exists in the SCHED 2 schedule only");
   constexpr int ROWB = 128;
   constexpr int HALF = 128 * ROWB;              // 16 KiB half-tile
   constexpr int BUF = 4 * HALF;                 // A0 A1 W0 W1
@@ -1041,7 +1045,48 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
   };
 
   const int nk = p.K / 64;
-  if constexpr (SCHED == 2) {
+  if constexpr (HN) {
+    // SCHED 2 with the W1 half dropped: phase A reads A0 W0 (quadrant (0,0)) and issues A1 of tile k+1, phase
+    // B reads A1 (quadrant (1,0)) and issues A0 W0 of tile k+2; every wait leaves the 6 youngest LDS-DMA
+    // (3 half-tiles) in flight.
+    issue(0, KA0);
+    issue(0, KW0);
+    issue(0, KA1);
+    if (nk > 1) {
+      issue(1, KA0);
+      issue(1, KW0);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
+    ln_prologue();
+    bar_raw();
+    if (wave >= 4) bar_raw();
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* buf = smem + (kt & 1) * BUF;
+      const bool m1 = kt + 1 < nk, m2 = kt + 2 < nk;
+      read_a(buf, 0);
+      read_w(buf, 0);
+      lds_done();
+      if (m1) { issue(kt + 1, KA1); asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }   // A1(kt)
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar_raw();
+      mma(0, 0);
+      bar_raw();
+      read_a(buf, 1);
+      lds_done();
+      if (m2) {
+        issue(kt + 2, KA0);
+        issue(kt + 2, KW0);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // A0 W0 (kt+1)
+      } else if (m1) {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      bar_raw();
+      mma(1, 0);
+      bar_raw();
+    }
+  } else if constexpr (SCHED == 2) {
     // 2 phases per K-tile: A (reads A0 W0 W1, quadrants (0,0) (0,1)) and B (reads A1, quadrants (1,0) (1,1)),
     // 32 MFMAs each.  Issue order: A0 W0 W1 of tile k+2 in B(k), A1 of tile k+1 in A(k); every wait leaves
     // the 8 youngest LDS-DMA (4 half-tiles) in flight.
@@ -1551,6 +1596,23 @@ static hipError_t launch8p(const GemmArgs& p, int epi, hipStream_t stream) {
   return hipGetLastError();
 }
 
+template <int CONV>
+static hipError_t launch8d_hn(const GemmArgs& p, int epi, hipStream_t stream) {
+  constexpr int SMEM = 2 * 4 * 128 * 128 + EPI_LDS_EXTRA + COL_LDS_BYTES;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm8d_kernel<EPI_BF16, CONV, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8d_kernel<EPI_F32, CONV, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr_set = true;
+  }
+  if (p.N > 128 || (epi != EPI_BF16 && epi != EPI_F32)) return hipErrorInvalidValue;
+  const int nwg = (p.M + BM2 - 1) / BM2;
+  dim3 grid(nwg, p.batch > 1 ? p.batch : 1), block(512);
+  if (epi == EPI_BF16) hipLaunchKernelGGL((gemm8d_kernel<EPI_BF16, CONV, 2, 1>), grid, block, SMEM, stream, p, 1, nwg);
+  else hipLaunchKernelGGL((gemm8d_kernel<EPI_F32, CONV, 2, 1>), grid, block, SMEM, stream, p, 1, nwg);
+  return hipGetLastError();
+}
+
 template <int CONV, int SCHED>
 static hipError_t launch8d(const GemmArgs& p, int epi, hipStream_t stream) {
   constexpr int SMEM = 2 * 4 * 128 * 128 + EPI_LDS_EXTRA + COL_LDS_BYTES;   // ring + LN rows + bias / colsum
@@ -1622,8 +1684,11 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
   p.raster = g_gemm_raster ? g_gemm_raster : (p.N >= 8 * BN2 ? 8 : 0);
   p.dbg_tile0 = g_gemm_dbg;
   int algo = g_gemm_algo;
-  // batched GEMMs (decoder AttnBlock q k^T and p v, 1024 rows per image at 256^2) count all batches' rows
-  if (algo == 0) algo = ((long long)p.M * (p.batch > 1 ? p.batch : 1) >= 4096 && p.N >= 256) ? 7 : 1;
+  const long long rows_all = (long long)p.M * (p.batch > 1 ? p.batch : 1);
+  // batched GEMMs (decoder AttnBlock q k^T and p v, 1024 rows per image at 256^2) count all batches' rows;
+  // N <= 128 with many rows (the decoder's 128-channel convs): the 256 x 128 half-N tile (algo 8)
+  if (algo == 0) algo = (rows_all >= 4096 && p.N >= 256) ? 7 : (rows_all >= 16384 && p.N > 96 && p.N <= 128) ? 8 : 1;
+  if (algo == 8 && (p.N > 128 || (epi != EPI_BF16 && epi != EPI_F32) || p.ln_stats || p.stats_out)) algo = 1;
   // the 256-tile bf16 epilogue stores 16-byte row chunks: needs N, ldo multiples of 8 and an aligned output
   if ((epi == EPI_BF16 || epi == EPI_GELU) && (p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))) algo = 1;
   if (epi == EPI_F32 && (p.N % 8 || p.ldr % 4 || ((uintptr_t)p.out_f32 & 15) ||
@@ -1633,6 +1698,32 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
     return launch_mx(p, epi, stream);
   }
   if (p.out_fp8) algo = 7;   // MXFP8 output lives in the 256-tile epilogue
+  // operands past the descriptor kernels' 2 GiB byte-offset range (e.g. a 32-image chunk of 512^2 x 256-channel
+  // conv inputs): split the rows into parts that fit -- whole images for a conv -- instead of dropping to the
+  // 128-tile kernel
+  if (algo >= 5 && !fits_rsrc(p) && p.batch <= 1 && p.a_rows_per_group == 0 && !p.out_fp8) {
+    const int hw = p.conv ? p.convH * p.convW : 1;
+    const int m1 = p.conv ? (p.M / hw / 2) * hw : ((p.M / 2 + BM2 - 1) / BM2) * BM2;
+    if (m1 > 0 && m1 < p.M) {
+      GemmArgs a = args, b = args;
+      a.M = m1;
+      b.M = p.M - m1;
+      if (p.conv) b.A1 += (size_t)(m1 / hw) * (p.convH >> p.conv_up) * (p.convW >> p.conv_up) * p.convC;
+      else {
+        b.A1 += (size_t)m1 * p.lda1;
+        if (b.A2) b.A2 += (size_t)m1 * p.lda2;
+      }
+      if (b.out_bf16) b.out_bf16 += (size_t)m1 * p.ldo;
+      if (b.out_f32) b.out_f32 += (size_t)m1 * p.ldr;
+      if (b.res_in) b.res_in += (size_t)m1 * p.ldri;
+      if (b.stats_out) b.stats_out += (size_t)m1 * p.stats_ld * 2;
+      if (b.ln_stats) b.ln_stats += (size_t)m1 * p.ln_ld * 2;
+      const hipError_t e = gemm_launch(a, epi, stream);
+      return e != hipSuccess ? e : gemm_launch(b, epi, stream);
+    }
+  }
+  if (algo == 8 && fits_rsrc(p)) return p.conv ? launch8d_hn<1>(p, epi, stream) : launch8d_hn<0>(p, epi, stream);
+  if (algo == 8) algo = 1;
   if (epi == EPI_RES) {      // the residual epilogue exists in the default 256-tile schedule and the 128 tile
     if (algo != 1 && fits_rsrc(p)) return launch8d<0, 2>(p, epi, stream);
     algo = 1;

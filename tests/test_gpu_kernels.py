@@ -85,13 +85,14 @@ def test_gemm_split_k(lib):
     assert rel(out, ref) < 2e-3
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("M,N,K", [(4133, 1000, 1024), (515, 768, 2048), (8192, 512, 128), (700, 264, 64),
-                                   (1100, 520, 192)])
+                                   (1100, 520, 192), (5000, 128, 1152), (700, 120, 64)])
 @pytest.mark.parametrize("epi", ["gelu", "f32acc_copy", "split"])
 def test_gemm_algos(lib, algo, M, N, K, epi):
     """Every tile policy (1: 128x128, 2/3: 256x256 ring, 4: 256x256 8-phase staggered, 5: 8-phase with the deep
-    descriptor-addressed LDS-DMA pipeline) on ragged M/N tails and short / odd K-tile counts."""
+    descriptor-addressed LDS-DMA pipeline, 6/7 its other schedules, 8: the 256x128 half-N tile, which N > 128
+    sends to the 128 tile) on ragged M/N tails and short / odd K-tile counts."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K + algo)
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
@@ -117,10 +118,11 @@ def test_gemm_algos(lib, algo, M, N, K, epi):
         lib.load().pdm_set_gemm_algo(0)
 
 
-@pytest.mark.parametrize("algo", [1, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("algo", [1, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("B,h,Cin,N,up,epi", [(2, 16, 64, 128, 0, "f32acc"), (1, 8, 128, 256, 1, "f32"),
                                               (3, 12, 64, 64, 0, "bf16"), (1, 32, 256, 256, 0, "f32"),
-                                              (2, 8, 128, 4, 0, "f32")])
+                                              (2, 8, 128, 4, 0, "f32"), (2, 24, 256, 128, 1, "bf16"),
+                                              (1, 40, 128, 128, 0, "f32acc")])
 def test_gemm_conv3x3(lib, algo, B, h, Cin, N, up, epi):
     """Implicit-GEMM conv3x3 mode (decoder ResnetBlock / Upsample convs, libs/autoencoder.py:35-50,110-141) for
     every tile policy: ragged M (B*H*W not a tile multiple), the folded nearest-x2 upsample and the residual
@@ -147,6 +149,30 @@ def test_gemm_conv3x3(lib, algo, B, h, Cin, N, up, epi):
             assert rel(out, ref + r0) < 2e-3
     finally:
         lib.load().pdm_set_gemm_algo(0)
+
+
+def test_gemm_rows_split_past_2gib(lib):
+    """Operands past the descriptor kernels' 2 GiB offset range are split into row parts (whole images for a
+    conv) by gemm_launch: the split result equals, bit for bit, the same kernel run on the parts' slices."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    # conv: 17 images of 256 x 256 x 256 channels nearest-x2 upsampled to 512^2 -> N = 128 (half-N tile),
+    # bf16 A1 = 17 * 512^2 * 256 * 2 B > 2 GiB when read at full resolution (no upsample)
+    x = torch.randn(17, 512, 512, 256, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(128, 256, 3, 3, device="cuda", generator=g) * (9 * 256) ** -0.5).bfloat16()
+    bias = torch.randn(128, device="cuda", generator=g)
+    full = lib.gemm_conv3x3(x, w, bias, lib.EPI_BF16).view(17, 512 * 512, 128)
+    for b in (0, 8, 16):
+        part = lib.gemm_conv3x3(x[b:b + 1].contiguous(), w, bias, lib.EPI_BF16).view(512 * 512, 128)
+        assert torch.equal(full[b], part)
+    del x, full
+    # plain GEMM: 1.1 M rows x K = 1024 bf16 (2.25 GB)
+    M, K, N = 1100 * 1024, 1024, 256
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w2 = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+    out = lib.gemm(a, w2, None, lib.EPI_F32)
+    for r0 in (0, 550 * 1024, M - 4096):
+        ref = lib.gemm(a[r0:r0 + 4096].contiguous(), w2, None, lib.EPI_F32)
+        assert torch.equal(out[r0:r0 + 4096], ref)
 
 
 @pytest.mark.parametrize("algo", [1, 3, 4, 5, 6, 7])
