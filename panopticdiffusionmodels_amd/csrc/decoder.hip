@@ -180,25 +180,40 @@ __global__ __launch_bounds__(256) void conv_in_kernel(const float* z, float inv_
   }
 }
 
-// row softmax of fp32 scores * scale -> bf16 probabilities (rows of n <= 4096), one block per row
+// row softmax of fp32 scores * scale -> bf16 probabilities (rows of n <= 4096), one block per row; the row is
+// read once into registers (16 values per thread; the three-pass form re-read it for the max, the sum and
+// the output: 1.38 ms for 32 x 4096 rows of 4096)
 __global__ __launch_bounds__(256) void softmax_rows_kernel(const float* s, bf16* p, int n, float scale) {
   const float* row = s + (size_t)blockIdx.x * n;
   bf16* out = p + (size_t)blockIdx.x * n;
   __shared__ float red[8];
+  float v[16];
   float m = -3.0e38f;
-  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, row[i] * scale);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int i = threadIdx.x + j * 256;
+    v[j] = i < n ? row[i] * scale : -3.0e38f;
+    m = fmaxf(m, v[j]);
+  }
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  __syncthreads();
   float sum = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) sum += __expf(row[i] * scale - m);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    v[j] = __expf(v[j] - m);   // 0 past n
+    sum += v[j];
+  }
   sum = wave_sum(sum);
   if ((threadIdx.x & 63) == 0) red[4 + (threadIdx.x >> 6)] = sum;
   __syncthreads();
   const float inv = 1.0f / ((red[4] + red[5]) + (red[6] + red[7]));
-  for (int i = threadIdx.x; i < n; i += 256) out[i] = (bf16)(__expf(row[i] * scale - m) * inv);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int i = threadIdx.x + j * 256;
+    if (i < n) out[i] = (bf16)(v[j] * inv);
+  }
 }
 
 // [B][n][ld] column block -> [B][C][n] transpose (bf16), 32x32 tiles through LDS
@@ -250,66 +265,57 @@ __global__ __launch_bounds__(256) void conv_out_kernel(const bf16* g, int B, int
   for (int o = 0; o < out_ch; ++o) img[((size_t)b * out_ch + o) * H * W + r] = acc[o] + bias[o];
 }
 
-// The same conv for C = 8 * LPP in {64, 128} (every shipped decoder): LPP consecutive lanes share one pixel and
-// each loads 16 contiguous bytes of it, so a wave-instruction reads whole 128-B lines (one pixel per lane read a
-// 16-B piece of 64 different lines per instruction, 4.2 ms for 32 images at 256^2).  A lane keeps its 8
-// channels' weights of one tap in registers across the wave's 16 pixel groups; the LPP partial sums of a pixel
-// are combined with xor-shuffles.
-template <int LPP>
-__global__ __launch_bounds__(256) void conv_out8_kernel(const bf16* g, int B, int H, int W, const bf16* w,
-                                                        const float* bias, float* img, int out_ch) {
-  constexpr int C = LPP * 8, NPG = 64 / LPP, IT = 16;
-  __shared__ f32x4 wl[9 * C];
-  for (int i = threadIdx.x; i < 9 * C; i += 256)
-    wl[i] = f32x4{(float)w[i], (float)w[9 * C + i], (float)w[18 * C + i], (float)w[27 * C + i]};
-  __syncthreads();
+// The same conv for C in {64, 128} (every shipped decoder) on the matrix cores: out[pixel][o] is a GEMM of the
+// 9 * C im2col row with a 9C x 16 weight block (o >= out_ch zero), one v_mfma_f32_16x16x32_bf16 per 32-channel
+// slice of a tap.  A block owns one output row of one image and walks it in 64-pixel segments (4 waves x 16
+// pixels); per segment the 3 x 66 halo of input pixels is staged in LDS once (every input pixel was re-read by
+// 9 taps from L2 in the VALU version: 4.7 ms for 32 images at 512^2) with each pixel's 16-byte channel chunks
+// XOR-swizzled by the pixel index, so the 16 lanes of an A-fragment read (16 consecutive pixels, one chunk)
+// hit distinct banks.  A lane keeps its B fragments (w[o = lane % 16][k-slice]) for the whole K in registers.
+template <int C>
+__global__ __launch_bounds__(256) void conv_out_mfma_kernel(const bf16* g, int H, int W, const bf16* w,
+                                                            const float* bias, float* img, int out_ch) {
+  constexpr int NQ = C / 8;                  // 16-byte chunks per pixel
+  constexpr int SW = (NQ < 16 ? NQ : 16) - 1;
+  constexpr int SEG = 64, PX = SEG + 2;      // output pixels per segment, staged pixels per row
+  constexpr int KS = 9 * C / 32;             // MFMA k-steps (a k-step never straddles a tap: C % 32 == 0)
+  __shared__ __attribute__((aligned(16))) bf16 tile[3 * PX * C];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int sub = lane / LPP, ch = (lane % LPP) * 8;
-  const long long npix = (long long)B * H * W;
-  const long long base = ((long long)blockIdx.x * 4 + wave) * (NPG * IT) + sub;
-  int pyx[IT];         // (y << 16) | x of the lane's pixel in group `it`, -1 past the end
-  long long prow[IT];  // first element of that pixel's image
+  const int y = blockIdx.x, b = blockIdx.y;
+  const int o = lane & 15, kq = (lane >> 4) * 8;
+  bf16x8 wf[KS];
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const long long p = base + it * NPG;
-    if (p < npix) {
-      const int b = (int)(p / ((long long)H * W)), r = (int)(p - (long long)b * H * W);
-      pyx[it] = ((r / W) << 16) | (r % W);
-      prow[it] = (long long)b * H * W;
-    } else {
-      pyx[it] = -1;
-      prow[it] = 0;
-    }
+  for (int ks = 0; ks < KS; ++ks) {
+    wf[ks] = bf16x8{};
+    if (o < out_ch) wf[ks] = *reinterpret_cast<const bf16x8*>(w + (size_t)o * 9 * C + ks * 32 + kq);
   }
-  f32x4 acc[IT];
+  const float bo = o < out_ch ? bias[o] : 0.f;
+  const bf16* gb = g + (size_t)b * H * W * C;
+  for (int x0 = 0; x0 < W; x0 += SEG) {
+    __syncthreads();   // the previous segment's fragment reads are done
+    for (int e = threadIdx.x; e < 3 * PX * NQ; e += 256) {
+      const int r = e / (PX * NQ), rem = e - r * (PX * NQ), px = rem / NQ, q = rem - px * NQ;
+      const int yy = y + r - 1, xx = x0 + px - 1;
+      i32x4 v = i32x4{0, 0, 0, 0};
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = *reinterpret_cast<const i32x4*>(gb + ((size_t)yy * W + xx) * C + q * 8);
+      *reinterpret_cast<i32x4*>(tile + ((r * PX + px) * NQ + (q ^ (px & SW))) * 8) = v;
+    }
+    __syncthreads();
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int it = 0; it < IT; ++it) acc[it] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int tap = 0; tap < 9; ++tap) {
-    const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-    f32x4 wv[8];
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3, dx = tap - (tap / 3) * 3;
+      const int px = wave * 16 + (lane & 15) + dx;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) wv[j] = wl[tap * C + ch + j];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int yy = (pyx[it] >> 16) + dy, xx = (pyx[it] & 0xffff) + dx;
-      if (pyx[it] >= 0 && yy >= 0 && yy < H && xx >= 0 && xx < W) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(g + (prow[it] + (long long)yy * W + xx) * C + ch);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[it] += (float)v[j] * wv[j];
+      for (int c0 = 0; c0 < C; c0 += 32) {
+        const int q = (c0 + kq) >> 3;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + ((dy * PX + px) * NQ + (q ^ (px & SW))) * 8);
+        acc = mfma16x16x32(a, wf[tap * (C / 32) + c0 / 32], acc);
       }
     }
-  }
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-#pragma unroll
-    for (int off = 1; off < LPP; off <<= 1)
-#pragma unroll
-      for (int o = 0; o < 4; ++o) acc[it][o] += __shfl_xor(acc[it][o], off, 64);
-    if (lane % LPP == 0 && pyx[it] >= 0) {
-      const long long p = base + it * NPG;
-      const int b = (int)(p / ((long long)H * W)), r = (int)(p - (long long)b * H * W);
-      for (int o = 0; o < out_ch; ++o) img[((size_t)b * out_ch + o) * H * W + r] = acc[it][o] + bias[o];
-    }
+    // D[pixel 4 * (lane / 16) + i][o = lane % 16]: 4 consecutive pixels of output channel o
+    if (o < out_ch)
+      *reinterpret_cast<f32x4*>(img + (((size_t)b * out_ch + o) * H + y) * W + x0 + wave * 16 + 4 * (lane >> 4)) = acc + bo;
   }
 }
 
@@ -378,6 +384,7 @@ struct DWork {
   float* X2;      // second residual buffer (nin shortcut / upsample output)
   bf16* G;        // bf16 conv input
   bf16* H;        // bf16 conv1 output
+  bf16* XB;       // bf16 copy of X for the next block's nin_shortcut, written by the producing conv's epilogue
   bf16* QKV;      // attention: [B*hw, 3C]
   float* S;       // attention scores [B, hw, hw]
   bf16* P;        // probabilities [B, hw, hw]
@@ -419,6 +426,7 @@ DWork dlayout(const pdm_decoder* d, int B, char* base) {
   w.X2 = (float*)take((size_t)B * maxe * 4);
   w.G = (bf16*)take((size_t)B * maxe * 2);
   w.H = (bf16*)take((size_t)B * maxe * 2);
+  w.XB = (bf16*)take((size_t)B * maxe * 2);
   w.QKV = (bf16*)take((size_t)B * hw * 3 * d->top_ch * 2);
   w.S = (float*)take((size_t)B * hw * hw * 4);
   w.P = (bf16*)take((size_t)B * hw * hw * 2);
@@ -477,8 +485,11 @@ int linear(const DCtx& c, const bf16* A, int M, int K, const bf16* W, const floa
   return PDM_OK;
 }
 
-// ResnetBlock (libs/autoencoder.py:75-134): X (fp32 NHWC, cin) -> X (cout) in place (or via X2 for nin)
-int resblock(const DCtx& c, float*& X, float*& X2, int B, int res, int cin, int cout, const std::string& p) {
+// ResnetBlock (libs/autoencoder.py:75-134): X (fp32 NHWC, cin) -> X (cout) in place (or via X2 for nin).
+// xb: bf16(X) already made by the epilogue that produced X (else the nin_shortcut casts X itself); copy_out:
+// where conv2's epilogue also stores bf16 of the block output (the next upsample conv's source), or null.
+int resblock(const DCtx& c, float*& X, float*& X2, int B, int res, int cin, int cout, const std::string& p,
+             const bf16* xb = nullptr, bf16* copy_out = nullptr) {
   const DWork& w = *c.w;
   const int P = res * res;
   D_TRY(groupnorm<float>(c, X, B, P, cin, p + ".norm1", w.G, true));
@@ -486,15 +497,18 @@ int resblock(const DCtx& c, float*& X, float*& X2, int B, int res, int cin, int 
   D_TRY(groupnorm<bf16>(c, w.H, B, P, cout, p + ".norm2", w.G, true));
   if (cin != cout) {
     // x = nin_shortcut(x): 1x1 conv = GEMM on a bf16 copy of x, into X2; then X2 += conv2(h)
-    D_HIP(pdm::cast_bf16_launch(X, w.H, (long long)B * P * cin, c.s));
-    D_TRY(linear(c, w.H, B * P, cin, c.d->w(p + ".nin_shortcut.weight"), c.d->f(p + ".nin_shortcut.bias"), cout,
+    if (!xb) {
+      D_HIP(pdm::cast_bf16_launch(X, w.H, (long long)B * P * cin, c.s));
+      xb = w.H;
+    }
+    D_TRY(linear(c, xb, B * P, cin, c.d->w(p + ".nin_shortcut.weight"), c.d->f(p + ".nin_shortcut.bias"), cout,
                  pdm::EPI_F32, nullptr, X2, 0));
-    D_TRY(conv3(c, w.G, B, res, cout, cout, p + ".conv2", pdm::EPI_F32, nullptr, X2, 1));
+    D_TRY(conv3(c, w.G, B, res, cout, cout, p + ".conv2", pdm::EPI_F32, copy_out, X2, 1));
     float* t = X;
     X = X2;
     X2 = t;
   } else {
-    D_TRY(conv3(c, w.G, B, res, cout, cout, p + ".conv2", pdm::EPI_F32, nullptr, X, 1));
+    D_TRY(conv3(c, w.G, B, res, cout, cout, p + ".conv2", pdm::EPI_F32, copy_out, X, 1));
   }
   return PDM_OK;
 }
@@ -642,17 +656,25 @@ int pdm_decoder_decode(pdm_decoder* d, const float* z, float* img, int B, void* 
   D_TRY(attnblock(c, X, B, res, T, "decoder.mid.attn_1"));
   D_TRY(resblock(c, X, X2, B, res, T, T, "decoder.mid.block_2"));
   int cin = T;
+  const bf16* xb = nullptr;   // bf16(X) from the epilogue that produced X, when the next block's nin needs it
   for (int lvl = d->nlev - 1; lvl >= 0; --lvl) {
     const int cout = d->cfg.ch * d->cfg.ch_mult[lvl];
     for (int b = 0; b <= d->cfg.num_res_blocks; ++b) {
-      D_TRY(resblock(c, X, X2, B, res, cin, cout, "decoder.up." + std::to_string(lvl) + ".block." + std::to_string(b)));
+      // the level's last block also stores bf16 of its output into H: the upsample conv's source (H is free
+      // once norm2 has consumed conv1's output)
+      bf16* cp = (b == d->cfg.num_res_blocks && lvl != 0) ? w.H : nullptr;
+      D_TRY(resblock(c, X, X2, B, res, cin, cout, "decoder.up." + std::to_string(lvl) + ".block." + std::to_string(b),
+                     cin != cout ? xb : nullptr, cp));
+      xb = nullptr;
       cin = cout;
     }
     if (lvl != 0) {  // nearest x2 upsample folded into the conv's source addressing (35-50)
-      D_HIP(pdm::cast_bf16_launch(X, w.G, (long long)B * res * res * cin, s));
       res *= 2;
-      D_TRY(conv3(c, w.G, B, res, cin, cin, "decoder.up." + std::to_string(lvl) + ".upsample.conv", pdm::EPI_F32,
-                  nullptr, X2, 0, 1));
+      const int next = d->cfg.ch * d->cfg.ch_mult[lvl - 1];
+      bf16* cp = next != cin ? w.XB : nullptr;   // the next level's first block changes width: its nin input
+      D_TRY(conv3(c, w.H, B, res, cin, cin, "decoder.up." + std::to_string(lvl) + ".upsample.conv", pdm::EPI_F32,
+                  cp, X2, 0, 1));
+      xb = cp;
       float* t = X;
       X = X2;
       X2 = t;
@@ -663,12 +685,12 @@ int pdm_decoder_decode(pdm_decoder* d, const float* z, float* img, int B, void* 
     const long long npix = (long long)B * res * res;
     const bf16* cw = d->w("decoder.conv_out.weight");
     const float* cb = d->f("decoder.conv_out.bias");
-    if (cin == 128)
-      hipLaunchKernelGGL(pdm::conv_out8_kernel<16>, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, w.G, B, res,
-                         res, cw, cb, img, d->cfg.out_ch);
-    else if (cin == 64)
-      hipLaunchKernelGGL(pdm::conv_out8_kernel<8>, dim3((unsigned)((npix + 511) / 512)), dim3(256), 0, s, w.G, B, res,
-                         res, cw, cb, img, d->cfg.out_ch);
+    if (cin == 128 && res % 64 == 0)
+      hipLaunchKernelGGL(pdm::conv_out_mfma_kernel<128>, dim3(res, B), dim3(256), 0, s, w.G, res, res, cw, cb, img,
+                         d->cfg.out_ch);
+    else if (cin == 64 && res % 64 == 0)
+      hipLaunchKernelGGL(pdm::conv_out_mfma_kernel<64>, dim3(res, B), dim3(256), 0, s, w.G, res, res, cw, cb, img,
+                         d->cfg.out_ch);
     else
       hipLaunchKernelGGL(pdm::conv_out_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 9 * cin * 16, s, w.G,
                          B, res, res, cin, cw, cb, img, d->cfg.out_ch);

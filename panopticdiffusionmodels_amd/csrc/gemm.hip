@@ -1685,9 +1685,11 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
   p.dbg_tile0 = g_gemm_dbg;
   int algo = g_gemm_algo;
   const long long rows_all = (long long)p.M * (p.batch > 1 ? p.batch : 1);
-  // batched GEMMs (decoder AttnBlock q k^T and p v, 1024 rows per image at 256^2) count all batches' rows;
-  // N <= 128 with many rows (the decoder's 128-channel convs): the 256 x 128 half-N tile (algo 8)
-  if (algo == 0) algo = (rows_all >= 4096 && p.N >= 256) ? 7 : (rows_all >= 16384 && p.N > 96 && p.N <= 128) ? 8 : 1;
+  // batched GEMMs (decoder AttnBlock q k^T and p v, 1024 rows per image at 256^2) count all batches' rows
+  // (the 256 x 128 half-N tile, algo 8, is kept as an option only: on the decoder's 128-channel 512^2 convs it
+  // measured 1069 us vs 1063 us for the 128-tile kernel -- both bound by the A-operand refetch per 128 output
+  // columns, tools/conv_bench.py, profiles/r03l/conv.log)
+  if (algo == 0) algo = (rows_all >= 4096 && p.N >= 256) ? 7 : 1;
   if (algo == 8 && (p.N > 128 || (epi != EPI_BF16 && epi != EPI_F32) || p.ln_stats || p.stats_out)) algo = 1;
   // the 256-tile bf16 epilogue stores 16-byte row chunks: needs N, ldo multiples of 8 and an aligned output
   if ((epi == EPI_BF16 || epi == EPI_GELU) && (p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))) algo = 1;

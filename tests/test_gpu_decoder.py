@@ -71,6 +71,19 @@ def test_decoder_latent64_vs_oracle(dev):
         assert rel(img[i:i + 1], autoencoder_ref.decode(sd, z[i:i + 1])) < TOL
 
 
+@pytest.mark.parametrize("latent", [32, 24])
+def test_decoder_c64_conv_out_vs_oracle(dev, latent):
+    """64-channel output level (ch 64, ch_mult 1 2): conv_out on the C = 64 MFMA kernel (latent 32 -> a 64^2 side,
+    a multiple of its 64-pixel segments) and on the VALU fallback (latent 24 -> 48^2), both vs the oracle."""
+    ae, sd = _ae(64, (1, 2), 1, 11, "random", latent)
+    g = torch.Generator().manual_seed(latent)
+    z = torch.randn(2, 4, latent, latent, generator=g)
+    img = ae.to(dev).decode(z.to(dev))
+    for i in range(2):
+        ref = autoencoder_ref.decode(sd, z[i:i + 1], ch_mult=(1, 2), num_res_blocks=1)
+        assert rel(img[i:i + 1], ref) < TOL
+
+
 def test_decoder_rejects_unsupported(dev):
     ae, _ = _ae(32, (1, 2), 1, 13, "random", 8)
     with pytest.raises(ValueError):
