@@ -42,7 +42,7 @@ int pdm_device_arch(char* buf, int len);
 /* Tile-policy overrides for A/B measurement (0 = automatic; the default everywhere).
  *   GEMM: 1 = 128x128, 2 = 256x256 BK32 ring, 3 = 256x256 BK64 ring, 4 = 256x256 8-phase staggered,
  *         5 / 6 / 7 = 256x256 LDS-DMA descriptor kernel (schedules 0 / 1 / 2; 7 is the automatic choice for
- *         N >= 256), 8 = its 256x128 half-N tile (N <= 128, bf16 / fp32 epilogues; never chosen automatically)
+ *         N >= 256), 8 = its 256x128 half-N tile, 9 = a 512x128 tall tile (both N <= 128, bf16 / fp32 epilogues)
  *   attention: 1 = streamed K/V per 64-query block, 2 / 3 = head-resident K/V with 2 / 3 query tiles per wave,
  *              4 = head-resident v2 (Dh 64), 7 = head-resident Dh 72 (64 + 8 split); 5/6, 8/9 = their load-only /
  *              math-only timing variants (wrong results) */

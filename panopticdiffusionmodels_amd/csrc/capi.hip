@@ -731,7 +731,7 @@ const char* pdm_last_error(void) { return g_err.c_str(); }
 int pdm_version(void) { return 1; }
 
 int pdm_set_gemm_algo(int algo) {
-  if (algo < 0 || algo > 8) return fail(PDM_ERR_ARG, "pdm_set_gemm_algo: algo must be 0 (auto) or 1..8");
+  if (algo < 0 || algo > 9) return fail(PDM_ERR_ARG, "pdm_set_gemm_algo: algo must be 0 (auto) or 1..9");
   pdm::gemm_set_algo(algo);
   return PDM_OK;
 }

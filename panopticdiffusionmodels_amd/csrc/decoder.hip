@@ -267,21 +267,27 @@ __global__ __launch_bounds__(256) void conv_out_kernel(const bf16* g, int B, int
 
 // The same conv for C in {64, 128} (every shipped decoder) on the matrix cores: out[pixel][o] is a GEMM of the
 // 9 * C im2col row with a 9C x 16 weight block (o >= out_ch zero), one v_mfma_f32_16x16x32_bf16 per 32-channel
-// slice of a tap.  A block owns one output row of one image and walks it in 64-pixel segments (4 waves x 16
-// pixels); per segment the 3 x 66 halo of input pixels is staged in LDS once (every input pixel was re-read by
-// 9 taps from L2 in the VALU version: 4.7 ms for 32 images at 512^2) with each pixel's 16-byte channel chunks
-// XOR-swizzled by the pixel index, so the 16 lanes of an A-fragment read (16 consecutive pixels, one chunk)
-// hit distinct banks.  A lane keeps its B fragments (w[o = lane % 16][k-slice]) for the whole K in registers.
+// slice of a tap.  A block owns two output rows of one image and walks them in 64-pixel segments (4 waves x 16
+// pixels x 2 rows); per segment the 4 x 66 halo of input pixels is staged in LDS once by LDS-DMA (every input
+// pixel was re-read by 9 taps from L2 in the VALU version: 4.7 ms for 32 images at 512^2; register-staged loads
+// with one load in flight per thread: 1.9 ms), each pixel's 16-byte channel chunks XOR-swizzled by the pixel
+// index so the 16 lanes of an A-fragment read (16 consecutive pixels, one chunk) hit distinct banks.  The DMA
+// writes lane-linearly, so the swizzle is applied to the SOURCE chunk; halo pixels outside the image read as
+// zeros through the buffer descriptor's range check.  Two blocks per CU (68 KiB of LDS each) overlap one's
+// staging with the other's MFMAs.  A lane keeps its B fragments (w[o = lane % 16][k-slice]) for the whole K in
+// registers.
 template <int C>
 __global__ __launch_bounds__(256) void conv_out_mfma_kernel(const bf16* g, int H, int W, const bf16* w,
                                                             const float* bias, float* img, int out_ch) {
   constexpr int NQ = C / 8;                  // 16-byte chunks per pixel
   constexpr int SW = (NQ < 16 ? NQ : 16) - 1;
   constexpr int SEG = 64, PX = SEG + 2;      // output pixels per segment, staged pixels per row
+  constexpr int SLOTS = 4 * PX * NQ;         // 16-byte LDS slots per segment (4 input rows)
   constexpr int KS = 9 * C / 32;             // MFMA k-steps (a k-step never straddles a tap: C % 32 == 0)
-  __shared__ __attribute__((aligned(16))) bf16 tile[3 * PX * C];
+  static_assert(SLOTS % 64 == 0, "every LDS-DMA wave-instruction lands 64 slots inside the tile");
+  __shared__ __attribute__((aligned(16))) bf16 tile[SLOTS * 8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int y = blockIdx.x, b = blockIdx.y;
+  const int y0 = blockIdx.x * 2, b = blockIdx.y;
   const int o = lane & 15, kq = (lane >> 4) * 8;
   bf16x8 wf[KS];
 #pragma unroll
@@ -290,18 +296,22 @@ __global__ __launch_bounds__(256) void conv_out_mfma_kernel(const bf16* g, int H
     if (o < out_ch) wf[ks] = *reinterpret_cast<const bf16x8*>(w + (size_t)o * 9 * C + ks * 32 + kq);
   }
   const float bo = o < out_ch ? bias[o] : 0.f;
-  const bf16* gb = g + (size_t)b * H * W * C;
+  const long long img_bytes = (long long)H * W * C * 2;
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(g + (size_t)b * H * W * C), 0, (int)(img_bytes < 0x7fffffffLL ? img_bytes : 0x7fffffffLL), 0x00020000);
   for (int x0 = 0; x0 < W; x0 += SEG) {
-    __syncthreads();   // the previous segment's fragment reads are done
-    for (int e = threadIdx.x; e < 3 * PX * NQ; e += 256) {
-      const int r = e / (PX * NQ), rem = e - r * (PX * NQ), px = rem / NQ, q = rem - px * NQ;
-      const int yy = y + r - 1, xx = x0 + px - 1;
-      i32x4 v = i32x4{0, 0, 0, 0};
-      if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = *reinterpret_cast<const i32x4*>(gb + ((size_t)yy * W + xx) * C + q * 8);
-      *reinterpret_cast<i32x4*>(tile + ((r * PX + px) * NQ + (q ^ (px & SW))) * 8) = v;
+    // slot e = (r * PX + px) * NQ + s holds logical chunk s ^ (px & SW) of input pixel (y0 - 1 + r, x0 - 1 + px)
+    for (int e0 = wave * 64; e0 < SLOTS; e0 += 256) {
+      const int e = e0 + lane;
+      const int r = e / (PX * NQ), rem = e - r * (PX * NQ), px = rem / NQ, sl = rem - px * NQ;
+      const int yy = y0 + r - 1, xx = x0 + px - 1;
+      const unsigned off = (e < SLOTS && yy >= 0 && yy < H && xx >= 0 && xx < W)
+                               ? (unsigned)((yy * W + xx) * C + ((sl ^ (px & SW)) << 3)) * 2u : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (PDM_LDS void*)(tile + e0 * 8), 16, (int)off, 0, 0, 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int dy = tap / 3, dx = tap - (tap / 3) * 3;
@@ -309,13 +319,20 @@ __global__ __launch_bounds__(256) void conv_out_mfma_kernel(const bf16* g, int H
 #pragma unroll
       for (int c0 = 0; c0 < C; c0 += 32) {
         const int q = (c0 + kq) >> 3;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + ((dy * PX + px) * NQ + (q ^ (px & SW))) * 8);
-        acc = mfma16x16x32(a, wf[tap * (C / 32) + c0 / 32], acc);
+        const int sw = (q ^ (px & SW)) * 8;
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(tile + (dy * PX + px) * NQ * 8 + sw);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(tile + ((dy + 1) * PX + px) * NQ * 8 + sw);
+        acc0 = mfma16x16x32(a0, wf[tap * (C / 32) + c0 / 32], acc0);
+        acc1 = mfma16x16x32(a1, wf[tap * (C / 32) + c0 / 32], acc1);
       }
     }
     // D[pixel 4 * (lane / 16) + i][o = lane % 16]: 4 consecutive pixels of output channel o
-    if (o < out_ch)
-      *reinterpret_cast<f32x4*>(img + (((size_t)b * out_ch + o) * H + y) * W + x0 + wave * 16 + 4 * (lane >> 4)) = acc + bo;
+    if (o < out_ch) {
+      float* op = img + (((size_t)b * out_ch + o) * H + y0) * W + x0 + wave * 16 + 4 * (lane >> 4);
+      *reinterpret_cast<f32x4*>(op) = acc0 + bo;
+      *reinterpret_cast<f32x4*>(op + W) = acc1 + bo;
+    }
+    __syncthreads();   // every wave is done reading the tile before the next segment restages it
   }
 }
 
@@ -686,10 +703,10 @@ int pdm_decoder_decode(pdm_decoder* d, const float* z, float* img, int B, void* 
     const bf16* cw = d->w("decoder.conv_out.weight");
     const float* cb = d->f("decoder.conv_out.bias");
     if (cin == 128 && res % 64 == 0)
-      hipLaunchKernelGGL(pdm::conv_out_mfma_kernel<128>, dim3(res, B), dim3(256), 0, s, w.G, res, res, cw, cb, img,
+      hipLaunchKernelGGL(pdm::conv_out_mfma_kernel<128>, dim3(res / 2, B), dim3(256), 0, s, w.G, res, res, cw, cb, img,
                          d->cfg.out_ch);
     else if (cin == 64 && res % 64 == 0)
-      hipLaunchKernelGGL(pdm::conv_out_mfma_kernel<64>, dim3(res, B), dim3(256), 0, s, w.G, res, res, cw, cb, img,
+      hipLaunchKernelGGL(pdm::conv_out_mfma_kernel<64>, dim3(res / 2, B), dim3(256), 0, s, w.G, res, res, cw, cb, img,
                          d->cfg.out_ch);
     else
       hipLaunchKernelGGL(pdm::conv_out_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 9 * cin * 16, s, w.G,

@@ -1192,6 +1192,210 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
 }
 
 // ------------------------------------------------------------------------------------------------
+// Tall tile for N <= 128 (algo 9; the decoder's 128-channel 512^2 convs): 512 x 128 per workgroup, 8 waves.
+// A 256 x 128 tile re-fetches its 32 KiB A K-tile for half the MFMA work of a 256 x 256 one and runs at the
+// same time per K-tile (tools/conv_bench.py: algo 8 ~ algo 1 ~ 0.58 PF on these convs), so the N = 128 GEMM
+// needs more rows per W panel instead: four 128-row A quarters share one W half-tile.  Every wave owns a 64 x 32
+// piece of each quarter -- the same 32 accumulators and fragment reads per MFMA as gemm8d.  Ring: 2 slots x
+// (A0 A1 A2 A3 W) x 16 KiB = the whole 160 KiB LDS (no LN / prologue-staged columns: bias is read in the
+// epilogue).  Per K-tile:
+//   phase A(k): reads A0 W A1 of tile k, issues A2 A3 of tile k+1        wait: A2 A3 (k)
+//   phase B(k): reads A2 A3 of tile k,   issues A0 W A1 of tile k+2      wait: A0 W A1 (k+1)
+// every wait leaving the 10 youngest LDS-DMA (5 16-KiB pieces) in flight.  Quarter q accumulates into the
+// 256x256 layout's quadrant slot (q & 1, q >> 1), so the epilogue runs twice through the 256-tile epilogue: rows
+// 0-255 from slots (*, 0) (slots (*, 1) sit at columns >= 128 >= N and are never stored), then, with the two
+// slot halves swapped, rows 256-511.
+template <int EPI, int CONV>
+__global__ __launch_bounds__(512, 1) void gemm8t_kernel(GemmArgs p, int nwg) {
+  constexpr int ROWB = 128;
+  constexpr int HALF = 128 * ROWB;              // 16 KiB piece
+  constexpr int BUF = 5 * HALF;                 // A0 A1 A2 A3 W
+  constexpr int KW = 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+  }
+  const int m0 = bid * 512;
+  const int ldw = p.ldw > 0 ? p.ldw : p.K;
+  long long a1_rows;
+  if (CONV) a1_rows = (long long)(p.M / (p.convH * p.convW)) * (p.convH >> p.conv_up) * (p.convW >> p.conv_up);
+  else a1_rows = p.M;
+  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(p.A1, a1_rows * (CONV ? p.convC : p.lda1) * 2);
+  const __amdgpu_buffer_rsrc_t ra2 = make_rsrc(p.A2 ? p.A2 : p.A1, p.A2 ? (long long)p.M * p.lda2 * 2 : 0);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.W, (long long)(p.N - 1) * ldw * 2 + (long long)p.K * 2);
+
+  const int prow = lane >> 3, pch = lane & 7;
+  unsigned a1off[4][2], a2off[4][2], woff[2], sbv[2];   // conv: only sbv (the swizzled chunk) and cpix
+  int cpix[4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + prow;
+    const unsigned sb = (unsigned)((pch ^ ((row >> 1) & 7)) * 16);
+    sbv[i] = sb;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int gm = m0 + h * 128 + row;
+      if constexpr (CONV) {
+        if (gm < p.M) {
+          const int hw = p.convH * p.convW, b = gm / hw, r = gm - b * hw, y = r / p.convW;
+          cpix[h][i] = ((b * p.convH + y) << 12) | (r - y * p.convW);
+        } else {
+          cpix[h][i] = -1;
+        }
+        a1off[h][i] = 0;
+        a2off[h][i] = 0;
+      } else {
+        a1off[h][i] = gm < p.M ? (unsigned)gm * (unsigned)(p.lda1 * 2) + sb : OOB;
+        a2off[h][i] = gm < p.M ? (unsigned)gm * (unsigned)(p.lda2 * 2) + sb : OOB;
+        cpix[h][i] = 0;
+      }
+    }
+    woff[i] = row < p.N ? (unsigned)row * (unsigned)(ldw * 2) + sb : OOB;
+  }
+
+  auto issue = [&](int kt, int kind) {
+    const int k0 = kt * 64;
+    char* dst = smem + (kt & 1) * BUF + kind * HALF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      PDM_LDS void* d = (PDM_LDS void*)(dst + (wave * 2 + i) * 1024);
+      if (kind == KW) {
+        dma16(rw, woff[i], k0 * 2, d);
+      } else if constexpr (CONV) {
+        const int tap = k0 / p.convC, ci0 = k0 - tap * p.convC;
+        const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+        const int pix = cpix[kind][i];
+        const int yy = ((pix >> 12) % p.convH) + dy, xx = (pix & 4095) + dx;
+        const int bb = (pix >> 12) / p.convH;
+        unsigned off = OOB;
+        if (pix >= 0 && yy >= 0 && yy < p.convH && xx >= 0 && xx < p.convW) {
+          const int sh = p.conv_up, Hs = p.convH >> sh, Ws = p.convW >> sh;
+          off = (unsigned)(((bb * Hs + (yy >> sh)) * Ws + (xx >> sh)) * p.convC) * 2u + sbv[i];
+        }
+        dma16(ra1, off, ci0 * 2, d);
+      } else {
+        if (k0 < p.K1) dma16(ra1, a1off[kind][i], k0 * 2, d);
+        else dma16(ra2, a2off[kind][i], (k0 - p.K1) * 2, d);
+      }
+    }
+  };
+
+  f32x4 acc[32];
+#pragma unroll
+  for (int f = 0; f < 32; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // every fragment a phase uses is read before its first barrier (waves 4-7 run one barrier behind, so a read
+  // after it could race the other half's refill of the slot): two quarters' A fragments + the W fragments
+  bf16x8 af[2][4][2];   // A fragments of the phase's two quarters: [quarter & 1][mi][k-sub]
+  bf16x8 wf[2][2];      // W fragments: [ni][k-sub]
+  auto read_a = [&](const char* buf, int q) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int row = wm * 64 + mi * 16 + (lane & 15);
+        af[q & 1][mi][ks] = *reinterpret_cast<const bf16x8*>(buf + q * HALF + swz_off<64>(row, ks * 4 + (lane >> 4)));
+      }
+  };
+  auto read_w = [&](const char* buf) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int row = wn * 32 + ni * 16 + (lane & 15);
+        wf[ni][ks] = *reinterpret_cast<const bf16x8*>(buf + KW * HALF + swz_off<64>(row, ks * 4 + (lane >> 4)));
+      }
+  };
+  auto lds_done = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mma = [&](int q) {   // quarter q -> quadrant slot (q & 1, q >> 1)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          f32x4& c = acc[(((q & 1) * 2 + (q >> 1)) * 2 + ni) * 4 + mi];
+          c = mfma16x16x32(wf[ni][ks], af[q & 1][mi][ks], c);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = p.K / 64;
+  issue(0, 0);
+  issue(0, KW);
+  issue(0, 1);
+  issue(0, 2);
+  issue(0, 3);
+  if (nk > 1) {
+    issue(1, 0);
+    issue(1, KW);
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");   // A0 W A1 (0)
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  bar_raw();
+  if (wave >= 4) bar_raw();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* buf = smem + (kt & 1) * BUF;
+    const bool m1 = kt + 1 < nk, m2 = kt + 2 < nk;
+    // phase A
+    read_a(buf, 0);
+    read_w(buf);
+    read_a(buf, 1);
+    lds_done();
+    if (m1) {
+      issue(kt + 1, 2);
+      issue(kt + 1, 3);
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");   // A2 A3 (kt)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar_raw();
+    mma(0);
+    mma(1);
+    bar_raw();
+    // phase B
+    read_a(buf, 2);
+    read_a(buf, 3);
+    lds_done();
+    if (m2) {
+      issue(kt + 2, 0);
+      issue(kt + 2, KW);
+      issue(kt + 2, 1);
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");   // A0 W A1 (kt+1)
+    } else if (m1) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    bar_raw();
+    mma(2);
+    mma(3);
+    bar_raw();
+  }
+  if (wave < 4) bar_raw();
+
+  epilogue256<EPI, 1>(p, acc, smem, m0, 0, tid, lane, wm, wn);
+  if (m0 + 256 < p.M) {
+    __syncthreads();   // the first half's LDS read-back is done before the second half is staged
+#pragma unroll
+    for (int f = 0; f < 32; ++f)
+      if (f & 8) {
+        const f32x4 t = acc[f];
+        acc[f] = acc[f ^ 8];
+        acc[f ^ 8] = t;
+      }
+    epilogue256<EPI, 1>(p, acc, smem, m0 + 256, 0, tid, lane, wm, wn);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // MXFP8 GEMM (algo 7 schedule, e4m3 operands with E8M0 block scales) on v_mfma_scale_f32_16x16x128_f8f6f4:
 // twice the bf16 MFMA rate.  A K-tile is 128 fp8 = 128-byte LDS rows, so staging, swizzle and fragment reads
 // are byte-for-byte those of the bf16 kernel (a lane's 32-byte fragment = chunks g and 4+g, g = lane >> 4,
@@ -1597,6 +1801,22 @@ static hipError_t launch8p(const GemmArgs& p, int epi, hipStream_t stream) {
 }
 
 template <int CONV>
+static hipError_t launch8t(const GemmArgs& p, int epi, hipStream_t stream) {
+  constexpr int SMEM = 2 * 5 * 128 * 128;   // 160 KiB
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm8t_kernel<EPI_BF16, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8t_kernel<EPI_F32, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr_set = true;
+  }
+  if (p.N > 128 || p.batch > 1 || (epi != EPI_BF16 && epi != EPI_F32)) return hipErrorInvalidValue;
+  const int nwg = (p.M + 511) / 512;
+  if (epi == EPI_BF16) hipLaunchKernelGGL((gemm8t_kernel<EPI_BF16, CONV>), dim3(nwg), dim3(512), SMEM, stream, p, nwg);
+  else hipLaunchKernelGGL((gemm8t_kernel<EPI_F32, CONV>), dim3(nwg), dim3(512), SMEM, stream, p, nwg);
+  return hipGetLastError();
+}
+
+template <int CONV>
 static hipError_t launch8d_hn(const GemmArgs& p, int epi, hipStream_t stream) {
   constexpr int SMEM = 2 * 4 * 128 * 128 + EPI_LDS_EXTRA + COL_LDS_BYTES;
   static bool attr_set = false;
@@ -1686,11 +1906,13 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
   int algo = g_gemm_algo;
   const long long rows_all = (long long)p.M * (p.batch > 1 ? p.batch : 1);
   // batched GEMMs (decoder AttnBlock q k^T and p v, 1024 rows per image at 256^2) count all batches' rows
-  // (the 256 x 128 half-N tile, algo 8, is kept as an option only: on the decoder's 128-channel 512^2 convs it
-  // measured 1069 us vs 1063 us for the 128-tile kernel -- both bound by the A-operand refetch per 128 output
-  // columns, tools/conv_bench.py, profiles/r03l/conv.log)
-  if (algo == 0) algo = (rows_all >= 4096 && p.N >= 256) ? 7 : 1;
-  if (algo == 8 && (p.N > 128 || (epi != EPI_BF16 && epi != EPI_F32) || p.ln_stats || p.stats_out)) algo = 1;
+  // 96 < N <= 128 with many rows (the decoder's 128-channel 512^2 convs and nin_shortcut): the 512 x 128 tall
+  // tile, algo 9 (conv 128 -> 128 at 512^2 x 8 images: 870 us vs 1059 us on the 128 tile; the 256 x 128 half-N
+  // tile, algo 8, measured 1070 us and is kept as an option only: tools/conv_bench.py, profiles/r03q)
+  if (algo == 0)
+    algo = (rows_all >= 4096 && p.N >= 256) ? 7 : (rows_all >= 65536 && p.N > 96 && p.N <= 128 && p.batch <= 1) ? 9 : 1;
+  if ((algo == 8 || algo == 9) && (p.N > 128 || (epi != EPI_BF16 && epi != EPI_F32) || p.ln_stats || p.stats_out ||
+                                    p.out_fp8 || p.a_rows_per_group > 0 || (algo == 9 && p.batch > 1))) algo = 1;
   // the 256-tile bf16 epilogue stores 16-byte row chunks: needs N, ldo multiples of 8 and an aligned output
   if ((epi == EPI_BF16 || epi == EPI_GELU) && (p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))) algo = 1;
   if (epi == EPI_F32 && (p.N % 8 || p.ldr % 4 || ((uintptr_t)p.out_f32 & 15) ||
@@ -1725,7 +1947,8 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
     }
   }
   if (algo == 8 && fits_rsrc(p)) return p.conv ? launch8d_hn<1>(p, epi, stream) : launch8d_hn<0>(p, epi, stream);
-  if (algo == 8) algo = 1;
+  if (algo == 9 && fits_rsrc(p)) return p.conv ? launch8t<1>(p, epi, stream) : launch8t<0>(p, epi, stream);
+  if (algo == 8 || algo == 9) algo = 1;
   if (epi == EPI_RES) {      // the residual epilogue exists in the default 256-tile schedule and the 128 tile
     if (algo != 1 && fits_rsrc(p)) return launch8d<0, 2>(p, epi, stream);
     algo = 1;

@@ -85,14 +85,14 @@ def test_gemm_split_k(lib):
     assert rel(out, ref) < 2e-3
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("M,N,K", [(4133, 1000, 1024), (515, 768, 2048), (8192, 512, 128), (700, 264, 64),
                                    (1100, 520, 192), (5000, 128, 1152), (700, 120, 64)])
 @pytest.mark.parametrize("epi", ["gelu", "f32acc_copy", "split"])
 def test_gemm_algos(lib, algo, M, N, K, epi):
     """Every tile policy (1: 128x128, 2/3: 256x256 ring, 4: 256x256 8-phase staggered, 5: 8-phase with the deep
-    descriptor-addressed LDS-DMA pipeline, 6/7 its other schedules, 8: the 256x128 half-N tile, which N > 128
-    sends to the 128 tile) on ragged M/N tails and short / odd K-tile counts."""
+    descriptor-addressed LDS-DMA pipeline, 6/7 its other schedules, 8 / 9: the 256x128 half-N / 512x128 tall
+    tiles, which N > 128 sends to the 128 tile) on ragged M/N tails and short / odd K-tile counts."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K + algo)
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
@@ -118,7 +118,7 @@ def test_gemm_algos(lib, algo, M, N, K, epi):
         lib.load().pdm_set_gemm_algo(0)
 
 
-@pytest.mark.parametrize("algo", [1, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("algo", [1, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("B,h,Cin,N,up,epi", [(2, 16, 64, 128, 0, "f32acc"), (1, 8, 128, 256, 1, "f32"),
                                               (3, 12, 64, 64, 0, "bf16"), (1, 32, 256, 256, 0, "f32"),
                                               (2, 8, 128, 4, 0, "f32"), (2, 24, 256, 128, 1, "bf16"),

@@ -39,7 +39,7 @@ for name, r, cin, cout, up, epi in shapes:
     acc = torch.zeros(B * R * R, cout, device=dev) if epi != "bf16" else None
     ob = torch.empty(B * R * R, cout, device=dev, dtype=torch.bfloat16) if epi == "bf16" else None
     line = f"{name:24s} B={B} M={B * R * R}"
-    for algo in [0, 1, 7, 8]:
+    for algo in [0, 1, 7, 8, 9]:
         lib.pdm_set_gemm_algo(algo)
         try:
             fn = (lambda: _lib.gemm_conv3x3(x, w, bias, _lib.EPI_BF16, up=up, out=ob)) if epi == "bf16" else \

@@ -1,5 +1,7 @@
+# rocprof evidence for every bench config (tools/profile_bench.sh), tag = $1 (default r03a)
 set -e
-bash tools/profile_bench.sh r03a imagenet256_uvit_large 95
-bash tools/profile_bench.sh r03a imagenet256_uvit_huge 95
-bash tools/profile_bench.sh r03a imagenet512_uvit_huge 95 fp8
-bash tools/profile_bench.sh r03a mscoco_uvit_small 64
+TAG=${1:-r03a}
+bash tools/profile_bench.sh $TAG imagenet256_uvit_large 95
+bash tools/profile_bench.sh $TAG imagenet256_uvit_huge 95
+bash tools/profile_bench.sh $TAG imagenet512_uvit_huge 95 fp8
+bash tools/profile_bench.sh $TAG mscoco_uvit_small 64
