@@ -866,10 +866,6 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
-  // timing experiment (bit 4): half of the first wave's workgroups start (dbg >> 8) x ~8k cycles late, so the
-  // CU halves run out of phase and their epilogue store bursts alternate
-  if ((p.dbg_tile0 & 16) && blockIdx.x < 256 && ((blockIdx.x >> 3) & 1))
-    for (int i = 0; i < ((p.dbg_tile0 >> 8) & 255); ++i) __builtin_amdgcn_s_sleep(127);
   int bid = blockIdx.x;
   {
     const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
