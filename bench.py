@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=95,
                     help="images per GPU per step (95: 2x95x258 token rows tile the 256-row GEMM tiles exactly)")
     ap.add_argument("--config", default="imagenet256_uvit_large")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="sample the batch as this many concurrent sub-batches on their own streams (fills the "
+                         "partly idle last GEMM wave of batches whose rows tile the 256-row GEMM unevenly)")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
@@ -114,14 +117,14 @@ def main():
                     v.zero_()
         clip = clip.to(dev)
         sampler = T2ISampler(net, cfg_scale=full["cfg_scale"], steps=full["sample_steps"],
-                             use_graph=not args.no_graph)
+                             use_graph=not args.no_graph, lanes=args.lanes)
         empty_ids = torch.full((1, 77), CLIP_EOS, dtype=torch.int64)
         empty_ids[0, 0] = CLIP_BOS
         empty_ctx = clip.encode_tokens(empty_ids.to(dev))[0]   # the dataset's empty_context (datasets.py:629)
     else:
         sampler = ClassCondSampler(net, front_end=full["front_end"], cfg_scale=full["cfg_scale"],
                                    null_label=null_label, steps=full["sample_steps"], eps=full.get("eps"),
-                                   use_graph=not args.no_graph)
+                                   use_graph=not args.no_graph, lanes=args.lanes)
     ae = get_model(None, scale_factor=full.get("scale_factor", 0.18215), seed=1).to(dev) if not args.no_decode else None
 
     # inputs for every (warmup + timed) step, generated per GLOBAL sample index and resident in HBM
@@ -226,7 +229,8 @@ def main():
         "config": {"workload": f"{args.config}: 50-step DPM-Solver (fast, order 3), CFG {full['cfg_scale']}, "
                                f"{f'+ KL-f8 decode {8 * zshape[-1]}x{8 * zshape[-1]}' if ae is not None else 'no decode'}",
                    "model": MODEL_NAMES.get(args.config, args.config), "per_gpu_batch": B, "global_batch": world * B,
-                   "nfe": sampler.nfe, "hip_graph": not args.no_graph, "parallelism": f"dp{world} (batch-sharded)"},
+                   "nfe": sampler.nfe, "hip_graph": not args.no_graph, "parallelism": f"dp{world} (batch-sharded)",
+                   "lanes": sampler.lanes},
         "roofline": roof,
         "end_to_end": None if tf_img is None or ae is None else {
             "algorithmic_tflop_per_image": tf_img, "achieved_tflops": round(value * tf_img, 1),

@@ -103,7 +103,8 @@ class UViT(HipNet):
             nat.packed[f"{key}.bias"] = layer.bias.detach().float().contiguous()
         return nat.packed[f"{key}.weight"], nat.packed[f"{key}.bias"]
 
-    def forward_pre(self, x, timesteps, context, mask_token=None, use_ground_truth=False, out=None, mask_out=None):
+    def forward_pre(self, x, timesteps, context, mask_token=None, use_ground_truth=False, out=None, mask_out=None,
+                    workspace=None):
         """Up to the heads: returns (eps_pre, mask_pre or None), both unpatchified, before conv / tanh."""
         _lib.require_gpu(x)
         nat = self.native()
@@ -126,7 +127,7 @@ class UViT(HipNet):
             out = torch.empty(B, self.in_chans, self.img_size, self.img_size, device=x.device)
         if mt is not None and not use_ground_truth and mask_out is None:
             mask_out = torch.empty(B, self.num_panoptic_class, self.img_size, self.img_size, device=x.device)
-        ws = nat.workspace(B, x.device)
+        ws = nat.workspace(B, x.device) if workspace is None else workspace   # a lane's private workspace
         _lib.check(nat.lib.pdm_uvit_t2i_forward(nat.h, _lib.ptr(x), _lib.ptr(t), _lib.ptr(context), _lib.ptr(mt),
                                                 int(bool(use_ground_truth)), _lib.ptr(out),
                                                 _lib.ptr(mask_out if mt is not None else None), B, _lib.ptr(ws),

@@ -56,24 +56,32 @@ class ClassCondSampler:
     """
 
     def __init__(self, nnet, front_end="dpm_solver_pytorch", cfg_scale=0.4, null_label=1000, steps=50, eps=None,
-                 betas=None, use_graph=True):
+                 betas=None, use_graph=True, lanes=1):
         self.nnet = nnet
         self.plan, self.time_scale = build_plan(front_end, steps, eps, betas)
         self.cfg = cfg_scale is not None and cfg_scale > 0
         self.cfg_scale = float(cfg_scale or 0.0)
         self.null_label = null_label
         self.use_graph = use_graph
+        # lanes > 1 (graph mode): the batch is cut into `lanes` sub-batches sampled concurrently on their own
+        # streams, each with a private workspace and graph, so one lane's GEMMs fill the CUs the other's leave
+        # idle in a partly filled last wave (batches whose 2B * L rows tile the 256-row GEMM unevenly)
+        self.lanes = max(1, int(lanes))
+        self._streams = []
         self._state = {}
         self.nfe = sc.nfe(self.plan)
 
-    def _buffers(self, B, device):
-        key = (B, device)
+    def _buffers(self, B, device, lane=None):
+        key = (B, device, lane)
         if key in self._state:
             return self._state[key]
         n = self.nnet
         rows = 2 * B if self.cfg else B
         shp = (n.in_chans, n.img_size, n.img_size)
         st = dict(
+            # a lane's private workspace (concurrent lanes must not share the handle's)
+            ws=None if lane is None else torch.empty(n.native().workspace_bytes(rows), dtype=torch.uint8,
+                                                     device=device),
             rows=rows,
             xin=torch.empty(rows, *shp, device=device),           # batched model input [cond | uncond]
             pre=torch.empty(rows, *shp, device=device),           # model output before the final conv
@@ -100,7 +108,7 @@ class ClassCondSampler:
         k = 0
         for stages in self.plan:
             for j, s in enumerate(stages):
-                n.forward_pre(xin, st["t"][k], st["y"], out=pre)
+                n.forward_pre(xin, st["t"][k], st["y"], out=pre, workspace=st["ws"])
                 last = j == len(stages) - 1
                 terms = [x] + ms[:j]
                 coeffs = [s["nx"]] + s["nm"]
@@ -115,7 +123,31 @@ class ClassCondSampler:
         eager=True runs this call without the HIP graph (e.g. with the GEMM profiling hook enabled)."""
         _lib.require_gpu(z)
         B = z.shape[0]
-        st = self._buffers(B, z.device)
+        if self.lanes > 1 and B >= self.lanes and self.use_graph and not eager:
+            return self._sample_lanes(z, y)
+        return self._sample_one(z, y, eager)
+
+    def _sample_lanes(self, z, y):
+        main = torch.cuda.current_stream(z.device)
+        while len(self._streams) < self.lanes:
+            self._streams.append(torch.cuda.Stream(device=z.device))
+        bounds = [round(i * z.shape[0] / self.lanes) for i in range(self.lanes + 1)]
+        outs = []
+        for i in range(self.lanes):
+            s = self._streams[i]
+            s.wait_stream(main)
+            with torch.cuda.stream(s):
+                zi = z[bounds[i]:bounds[i + 1]]
+                yi = y[bounds[i]:bounds[i + 1]] if y is not None else None
+                outs.append(self._sample_one(zi, yi, False, lane=i))
+        for i, o in enumerate(outs):
+            main.wait_stream(self._streams[i])
+            o.record_stream(main)
+        return torch.cat(outs)
+
+    def _sample_one(self, z, y, eager, lane=None):
+        B = z.shape[0]
+        st = self._buffers(B, z.device, lane)
         st["x"].copy_(z)
         st["xin"][:B].copy_(z)
         if self.cfg:
@@ -152,8 +184,10 @@ class T2ISampler:
     betas, CFG on both the noise and the predicted mask (uncond = empty_context), mask co-update with
     `enable_mask_opt`.  Returns (z_0, pred_mask)."""
 
-    def __init__(self, nnet, cfg_scale=1.0, steps=50, betas=None, enable_mask_opt=True, use_graph=True):
+    def __init__(self, nnet, cfg_scale=1.0, steps=50, betas=None, enable_mask_opt=True, use_graph=True, lanes=1):
         self.nnet = nnet
+        self.lanes = max(1, int(lanes))   # concurrent sub-batches (ClassCondSampler)
+        self._streams = []
         hs = sc.HostDiscrete(betas=sd_betas() if betas is None else betas)
         self.plan = sc.pp_fast_plan(hs, steps, 1.0 / hs.N, 1.0, order=3, predict_x0=True,
                                     enable_mask_opt=enable_mask_opt)
@@ -164,8 +198,8 @@ class T2ISampler:
         self.nfe = sc.nfe(self.plan)
         self._state = {}
 
-    def _buffers(self, B, device):
-        key = (B, device)
+    def _buffers(self, B, device, lane=None):
+        key = (B, device, lane)
         if key in self._state:
             return self._state[key]
         n = self.nnet
@@ -173,6 +207,8 @@ class T2ISampler:
         S, K = n.img_size, n.num_panoptic_class
         shp, mshp = (n.in_chans, S, S), (K, S, S)
         st = dict(
+            ws=None if lane is None else torch.empty(n.native().workspace_bytes(rows), dtype=torch.uint8,
+                                                     device=device),
             xin=torch.empty(rows, *shp, device=device), pre=torch.empty(rows, *shp, device=device),
             x=torch.empty(B, *shp, device=device), m=[torch.empty(B, *shp, device=device) for _ in range(3)],
             min=torch.empty(rows, *mshp, device=device), mpre=torch.empty(rows, *mshp, device=device),
@@ -197,7 +233,7 @@ class T2ISampler:
         k = 0
         for stages in self.plan:
             for j, s in enumerate(stages):
-                n.forward_pre(xin, st["t"][k], st["ctx"], mn, out=st["pre"], mask_out=st["mpre"])
+                n.forward_pre(xin, st["t"][k], st["ctx"], mn, out=st["pre"], mask_out=st["mpre"], workspace=st["ws"])
                 last = j == len(stages) - 1
                 _lib.stage_epilogue(st["pre"], B, conv_w=wx, conv_b=bx, cfg_scale=scale, xin=xin[:B], ax=s["ax"],
                                     ae=s["ae"], m_out=ms[j], terms=[x] + ms[:j], coeffs=[s["nx"]] + s["nm"],
@@ -217,7 +253,28 @@ class T2ISampler:
     def sample(self, z, context, empty_context, mask_token):
         _lib.require_gpu(z)
         B = z.shape[0]
-        st = self._buffers(B, z.device)
+        if self.lanes > 1 and B >= self.lanes and self.use_graph:
+            main = torch.cuda.current_stream(z.device)
+            while len(self._streams) < self.lanes:
+                self._streams.append(torch.cuda.Stream(device=z.device))
+            bounds = [round(i * B / self.lanes) for i in range(self.lanes + 1)]
+            outs = []
+            for i in range(self.lanes):
+                s = self._streams[i]
+                s.wait_stream(main)
+                lo, hi = bounds[i], bounds[i + 1]
+                with torch.cuda.stream(s):
+                    outs.append(self._sample_one(z[lo:hi], context[lo:hi], empty_context, mask_token[lo:hi], i))
+            for i, (a, b) in enumerate(outs):
+                main.wait_stream(self._streams[i])
+                a.record_stream(main)
+                b.record_stream(main)
+            return torch.cat([a for a, _ in outs]), torch.cat([b for _, b in outs])
+        return self._sample_one(z, context, empty_context, mask_token)
+
+    def _sample_one(self, z, context, empty_context, mask_token, lane=None):
+        B = z.shape[0]
+        st = self._buffers(B, z.device, lane)
 
         def load():
             st["x"].copy_(z)

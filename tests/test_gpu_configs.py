@@ -101,6 +101,10 @@ def test_full_t2i_sampler_properties(dev, coco):
     assert torch.equal(a, b) and torch.equal(pa, pb)
     c, pc = se.sample(z[:1], ctx[:1], empty, mt[:1])
     assert rel(c, a[:1]) < 1e-6 and rel(pc, pa[:1]) < 1e-6
+    # concurrent sub-batch lanes (two streams, private workspaces / graphs) give the single-lane result
+    s2 = T2ISampler(net, cfg_scale=scale, steps=50, use_graph=True, lanes=2)
+    d, pd = s2.sample(z, ctx, empty, mt)
+    assert rel(d, a) < 1e-6 and rel(pd, pa) < 1e-6
 
 
 @pytest.mark.parametrize("name,B", [("imagenet256_uvit_huge", 3), ("imagenet512_uvit_huge", 2)])
