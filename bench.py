@@ -48,10 +48,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=95,
-                    help="images per GPU per step (95: 2x95x258 token rows tile the 256-row GEMM tiles exactly)")
+    ap.add_argument("--batch", type=int, default=50,
+                    help="images per GPU per step (default: the reference's mini_batch_size, "
+                         "configs/imagenet256_uvit_large.py:66)")
     ap.add_argument("--config", default="imagenet256_uvit_large")
-    ap.add_argument("--lanes", type=int, default=1,
+    ap.add_argument("--lanes", type=int, default=2,
                     help="sample the batch as this many concurrent sub-batches on their own streams (fills the "
                          "partly idle last GEMM wave of batches whose rows tile the 256-row GEMM unevenly)")
     ap.add_argument("--no-decode", action="store_true")
