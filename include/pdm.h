@@ -294,6 +294,49 @@ int pdm_clip_workspace_size(const pdm_clip* c, int batch, size_t* bytes);
 int pdm_clip_encode(pdm_clip* c, const int64_t* ids, int batch, int L, float* out, void* workspace,
                     size_t workspace_bytes, void* stream);
 
+/* ---- training step: LSimple (sde.py:270-279, train_ldm_discrete.py:87-90) + AdamW + EMA (train_ldm_discrete.py:
+ * 159-175, utils.py:308-345) of the class-conditional / unconditional U-ViT (libs/uvit.py; head dim 64, <= 288
+ * tokens per image, mlp_time_embed = False) -------------------------------------------------------------------
+ * All parameters live in one caller-owned flat fp32 buffer; pdm_train_param_info gives each reference state_dict
+ * key its element offset and count (256-B aligned, ordered head / out-blocks last..first / mid / in-blocks
+ * last..first / embeddings, so each block's gradients are one contiguous range).  The caller also owns a gradient
+ * buffer of the same size and layout, two bf16 buffers (the working copy, n_params elements, and the transposed
+ * block Linear weights, n_wt elements) and, for the optimizer, moments m, v and the EMA copy (n_params each). */
+typedef struct pdm_trainer pdm_trainer;
+int pdm_train_create(const pdm_uvit_cfg* cfg, pdm_trainer** out);
+int pdm_train_destroy(pdm_trainer* t);
+int pdm_train_param_count(const pdm_trainer* t);
+int pdm_train_param_info(const pdm_trainer* t, int i, char* name, int len, long long* offset, long long* numel);
+int pdm_train_sizes(const pdm_trainer* t, long long* n_params, long long* n_wt);
+int pdm_train_set_buffers(pdm_trainer* t, float* params, float* grads, void* wb, void* wt);
+/* bf16 working copies from the fp32 parameters (after loading them; pdm_train_adamw refreshes them itself) */
+int pdm_train_refresh(pdm_trainer* t, void* stream);
+int pdm_train_workspace_size(const pdm_trainer* t, int rows, size_t* bytes);
+/* replaces loss = LSimple(...); loss.mean().backward() for one batch of `rows` samples: xt [rows, C, H, W] the noised
+ * input, tvals [rows] the timesteps as the net receives them (n, or t * 999 for the ScoreModel), y [rows] int64 labels
+ * (NULL for an unconditional net), target [rows, C, H, W] the noise.  Writes loss[rows] = mos(target - nnet(xt)) and
+ * into the gradient buffer d(gscale * sum(loss)) / d(params) (gscale = 1 / rows: loss.mean()).  The forward keeps
+ * its activations in the workspace (bf16 GEMM operands, fp32 residual stream). */
+int pdm_train_step(pdm_trainer* t, const float* xt, const float* tvals, const int64_t* y, const float* target,
+                   float* loss, int rows, float gscale, void* workspace, size_t workspace_bytes, void* stream);
+/* torch.optim.AdamW step `step` (>= 1, bias corrections 1 - beta^step) over every parameter with the gradient buffer,
+ * then ema = ema_rate * ema + (1 - ema_rate) * params (utils.ema; ema may be NULL) and the bf16 copies */
+int pdm_train_adamw(pdm_trainer* t, float* m, float* v, float* ema, float lr, float beta1, float beta2, float eps,
+                    float weight_decay, int step, float ema_rate, void* stream);
+/* the backward kernels on their own (parity tests).  pdm_wgrad: C[n][k] (+)= sum_m A[m][n] B[m][k] (bf16 A [M][lda],
+ * B [M][ldb], fp32 C [N][ldc]; scratch for split-reduction partials, may be NULL).  pdm_attention_backward: softmax
+ * attention over packed qkv [B*L][3*H*Dh] with output o [B*L][H*Dh] and its gradient dout -> dqkv (Dh 64, L <= 288).
+ * pdm_layernorm_backward: nn.LayerNorm(D) over fp32 rows x, dh the output gradient (fp32, or bf16 if dh_bf16) ->
+ * dx (+= if accumulate), optional bf16 copy dxb, dgamma, dbeta (written); scratch >= (4 ceil(rows/4) + 1) 8 D bytes
+ * is plenty. */
+int pdm_wgrad(const void* A, int lda, const void* B, int ldb, float* C, int ldc, int M, int N, int K, int accumulate,
+              float* scratch, size_t scratch_bytes, void* stream);
+int pdm_attention_backward(const void* qkv, const void* o, const void* dout, void* dqkv, int B, int L, int H, int Dh,
+                           void* stream);
+int pdm_layernorm_backward(const float* x, const void* dh, int dh_bf16, const float* gamma, float* dx, void* dxb,
+                           float* dgamma, float* dbeta, int rows, int D, int accumulate, float* scratch,
+                           size_t scratch_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

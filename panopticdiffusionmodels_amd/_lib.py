@@ -149,6 +149,33 @@ _SIGS = {
     "pdm_decoder_workspace_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "pdm_decoder_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    # training step (include/pdm.h "training")
+    "pdm_train_create": (ctypes.c_int, [ctypes.POINTER(PdmUvitCfg), ctypes.POINTER(ctypes.c_void_p)]),
+    "pdm_train_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "pdm_train_param_count": (ctypes.c_int, [ctypes.c_void_p]),
+    "pdm_train_param_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong)]),
+    "pdm_train_sizes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong),
+                                       ctypes.POINTER(ctypes.c_longlong)]),
+    "pdm_train_set_buffers": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p]),
+    "pdm_train_refresh": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "pdm_train_workspace_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
+    "pdm_train_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p,
+                                      ctypes.c_size_t, ctypes.c_void_p]),
+    "pdm_train_adamw": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                       ctypes.c_int, ctypes.c_float, ctypes.c_void_p]),
+    "pdm_wgrad": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                 ctypes.c_size_t, ctypes.c_void_p]),
+    "pdm_attention_backward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    "pdm_layernorm_backward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_size_t, ctypes.c_void_p]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -446,6 +473,49 @@ def stage_epilogue(pre, B, conv_w=None, conv_b=None, cfg_scale=None, act_tanh=Fa
     a.x_out2 = x_out2.data_ptr() if x_out2 is not None else None
     a.x_out3 = x_out3.data_ptr() if x_out3 is not None else None
     check(lib.pdm_stage_epilogue(ctypes.byref(a), stream_ptr(pre.device)), "pdm_stage_epilogue")
+
+
+def wgrad(dy, x, out=None, accumulate=False, scratch_mb=64):
+    """Weight gradient dW = dy^T @ x (fp32 [N, K]) of bf16 rows dy [M, N], x [M, K] (pdm_wgrad)."""
+    lib = load()
+    require_gpu(dy)
+    M, N = dy.shape
+    K = x.shape[1]
+    if out is None:
+        out = torch.zeros(N, K, dtype=torch.float32, device=dy.device)
+    scratch = torch.empty(scratch_mb << 18, dtype=torch.float32, device=dy.device) if scratch_mb else None
+    check(lib.pdm_wgrad(ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(out), out.stride(0), M, N, K, int(accumulate),
+                        ptr(scratch), scratch.numel() * 4 if scratch is not None else 0, stream_ptr(dy.device)),
+          "pdm_wgrad")
+    return out
+
+
+def attention_backward(qkv, o, dout, B, L, H, Dh=64):
+    """d qkv (bf16 [B*L, 3*H*Dh]) of softmax attention (scale Dh^-0.5) from the forward's packed qkv, its output o
+    and the output gradient dout (pdm_attention_backward)."""
+    lib = load()
+    require_gpu(qkv)
+    dqkv = torch.empty_like(qkv)
+    check(lib.pdm_attention_backward(ptr(qkv), ptr(o), ptr(dout), ptr(dqkv), B, L, H, Dh, stream_ptr(qkv.device)),
+          "pdm_attention_backward")
+    return dqkv
+
+
+def layernorm_backward(x, dh, gamma, dx=None, accumulate=False):
+    """(dx fp32, dx bf16, dgamma, dbeta) of nn.LayerNorm(D) over fp32 rows x with output gradient dh (fp32 / bf16)."""
+    lib = load()
+    require_gpu(x)
+    rows, D = x.shape
+    if dx is None:
+        dx = torch.zeros(rows, D, dtype=torch.float32, device=x.device)
+    dxb = torch.empty(rows, D, dtype=torch.bfloat16, device=x.device)
+    dg = torch.empty(D, dtype=torch.float32, device=x.device)
+    db = torch.empty(D, dtype=torch.float32, device=x.device)
+    scratch = torch.empty((4 * ((rows + 3) // 4) + 8) * 2 * D, dtype=torch.float32, device=x.device)
+    check(lib.pdm_layernorm_backward(ptr(x), ptr(dh), int(dh.dtype == torch.bfloat16), ptr(gamma), ptr(dx), ptr(dxb),
+                                     ptr(dg), ptr(db), rows, D, int(accumulate), ptr(scratch), scratch.numel() * 4,
+                                     stream_ptr(x.device)), "pdm_layernorm_backward")
+    return dx, dxb, dg, db
 
 
 class GemmProfiler:

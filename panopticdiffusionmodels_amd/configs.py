@@ -25,6 +25,10 @@ CONFIGS = {
                   use_checkpoint=True),
         z_shape=(4, 32, 32), front_end="dpm_solver_pytorch", cfg_scale=0.4, decode=True,
         scale_factor=0.18215, sample_steps=50, eps=1e-4, mini_batch_size=50,
+        # training (configs/imagenet256_uvit_large.py:19-40,57-60; train_ldm.py: sde.LSimple, noise_pred)
+        train=dict(batch_size=1024, objective="sde", p_uncond=0.15, ema_rate=0.9999),
+        optimizer=dict(name="adamw", lr=0.0002, weight_decay=0.03, betas=(0.99, 0.99)),
+        lr_scheduler=dict(name="customized", warmup_steps=5000),
     ),
     "imagenet256_uvit_huge": dict(
         nnet=dict(name="uvit", img_size=32, patch_size=2, in_chans=4, embed_dim=1152, depth=28,
@@ -68,6 +72,24 @@ CONFIGS = {
                   num_heads=2, mlp_ratio=4, qkv_bias=False, mlp_time_embed=False, num_classes=-1),
         z_shape=(3, 16, 16), front_end="dpm_solver_pytorch", cfg_scale=0.0, decode=False,
         sample_steps=50, eps=1e-4, mini_batch_size=2,
+    ),
+    "tiny_uvit_train": dict(  # training-step fixtures: Dh = 64 (the attention backward), L = 2 + 64, conv
+        nnet=dict(name="uvit", img_size=16, patch_size=2, in_chans=4, embed_dim=64, depth=2,
+                  num_heads=1, mlp_ratio=4, qkv_bias=False, mlp_time_embed=False, num_classes=11),
+        z_shape=(4, 16, 16), front_end="dpm_solver_pytorch", cfg_scale=0.4, decode=False,
+        sample_steps=50, eps=1e-4, mini_batch_size=2,
+        train=dict(batch_size=4, objective="discrete", p_uncond=0.15, ema_rate=0.9),
+        optimizer=dict(name="adamw", lr=0.0002, weight_decay=0.03, betas=(0.99, 0.99)),
+        lr_scheduler=dict(name="customized", warmup_steps=5),
+    ),
+    "tiny_uvit_train_uncond": dict(  # unconditional (no label token), qkv bias, no final conv
+        nnet=dict(name="uvit", img_size=16, patch_size=2, in_chans=3, embed_dim=64, depth=2,
+                  num_heads=1, mlp_ratio=4, qkv_bias=True, mlp_time_embed=False, num_classes=-1, conv=False),
+        z_shape=(3, 16, 16), front_end="dpm_solver_pytorch", cfg_scale=0.0, decode=False,
+        sample_steps=50, eps=1e-4, mini_batch_size=2,
+        train=dict(batch_size=4, objective="sde", p_uncond=0.0, ema_rate=0.9),
+        optimizer=dict(name="adamw", lr=0.0002, weight_decay=0.03, betas=(0.99, 0.999)),
+        lr_scheduler=dict(name="customized", warmup_steps=-1),
     ),
     "tiny_t2i": dict(  # panoptic co-generation, separate streams
         nnet=dict(name="uvit_t2i", img_size=16, in_chans=4, patch_size=2, embed_dim=64, depth=2,

@@ -1,0 +1,242 @@
+"""LSimple training step on the HIP path.
+
+Restates, behind the reference's own names, what one training iteration does:
+  * `Schedule` / `stable_diffusion_beta_schedule` / `LSimple` — train_ldm_discrete.py:23-27,54-90 (discrete SD
+    betas, n ~ U{1..1000}, xn = sqrt(a_n) x0 + sqrt(1 - a_n) eps, loss = mos(eps - nnet(xn, n, y)));
+  * `LSimple_sde` — sde.py:64-69,270-279 with ScoreModel.noise_pred (sde.py:168-184): t ~ U(0, 1), the VPSDE
+    marginal, the net sees t * 999 (train_ldm.py, the U-ViT-L/2 config);
+  * `HipTrainState.train_step` — train_ldm_discrete.py:159-175: zero_grad, loss.mean().backward(), AdamW step
+    (utils.get_optimizer, torch.optim.AdamW semantics), the `customized` warm-up LR (utils.py:319-326), then the
+    EMA update (utils.py:339-345, rate config.ema_rate, default 0.9999);
+  * label dropout for classifier-free guidance — datasets.py:45-61 CFGDataset (p_uncond, the null label).
+The noise draw (n / t, eps) is host-side torch RNG, as in the reference; the network forward, the loss, the whole
+backward and the optimizer run on libpdm's HIP kernels (csrc/train.hip, csrc/train_kernels.hip).  Data parallel:
+one process per GPU, the gradient buffer all-reduced (average, RCCL) between backward and optimizer step — the
+DDP semantics accelerate gives the reference (train_ldm_discrete.py:130-132).
+"""
+import ctypes
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .native import cfg_struct
+from .sde import VPSDE, mos, stp
+
+
+def stable_diffusion_beta_schedule(linear_start=0.00085, linear_end=0.0120, n_timestep=1000):
+    """train_ldm_discrete.py:23-27."""
+    return (torch.linspace(linear_start ** 0.5, linear_end ** 0.5, n_timestep, dtype=torch.float64) ** 2).numpy()
+
+
+class Schedule:
+    """Discrete-time forward process (train_ldm_discrete.py:54-84): betas[0] = 0, cum_alphas = prod(1 - betas)."""
+
+    def __init__(self, _betas):
+        self._betas = _betas
+        self.betas = np.append(0., _betas)
+        self.alphas = 1. - self.betas
+        self.N = len(_betas)
+        self.cum_alphas = self.alphas.cumprod()
+        self.cum_betas = 1. - self.cum_alphas
+
+    def sample(self, x0, rng=None):
+        """(n, eps, xn), n uniform in {1..N} (np.random.choice as the reference; `rng` a numpy Generator /
+        RandomState for reproducible draws), eps ~ N(0, 1)."""
+        choice = (rng or np.random).choice
+        n = choice(list(range(1, self.N + 1)), (len(x0),))
+        eps = torch.randn_like(x0)
+        xn = stp(self.cum_alphas[n] ** 0.5, x0) + stp(self.cum_betas[n] ** 0.5, eps)
+        return torch.tensor(n, device=x0.device), eps, xn
+
+
+def drop_labels(y, p_uncond, null_label, generator=None):
+    """CFGDataset (datasets.py:45-61): each label replaced by the null class with probability p_uncond."""
+    if not p_uncond:
+        return y
+    r = torch.rand(y.shape, generator=generator, device=y.device if generator is None else "cpu").to(y.device)
+    return torch.where(r < p_uncond, torch.full_like(y, null_label), y)
+
+
+def customized_lr(base_lr, step, warmup_steps=-1):
+    """utils.customized_lr_scheduler (utils.py:319-326): LambdaLR factor min(step / warmup, 1) at scheduler step
+    `step` (the number of optimizer steps already taken)."""
+    return base_lr * (min(step / warmup_steps, 1) if warmup_steps > 0 else 1)
+
+
+class HipTrainState:
+    """Parameters, gradients, AdamW moments and the EMA copy of one U-ViT in flat device buffers (pdm_train_*).
+
+    `state_dict()` / `ema_state_dict()` hand back reference-keyed tensors (views copied out), so checkpoints
+    interoperate with utils.TrainState's nnet / nnet_ema files."""
+
+    def __init__(self, nnet_kwargs, device="cuda", optimizer=None, lr_scheduler=None, ema_rate=0.9999):
+        _lib.require_gpu()
+        kw = dict(nnet_kwargs)
+        if kw.pop("name", "uvit") != "uvit":
+            raise ValueError("HipTrainState: the class-conditional / unconditional U-ViT (libs/uvit.py) only")
+        self.kw = kw
+        self.device = torch.device(device)
+        self.lib = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.pdm_train_create(ctypes.byref(cfg_struct(kw, False)), ctypes.byref(h)), "pdm_train_create")
+        self.h = h
+        n, nwt = ctypes.c_longlong(), ctypes.c_longlong()
+        _lib.check(self.lib.pdm_train_sizes(h, ctypes.byref(n), ctypes.byref(nwt)), "pdm_train_sizes")
+        self.n = n.value
+        self.index = {}
+        buf = ctypes.create_string_buffer(256)
+        for i in range(self.lib.pdm_train_param_count(h)):
+            off, numel = ctypes.c_longlong(), ctypes.c_longlong()
+            _lib.check(self.lib.pdm_train_param_info(h, i, buf, 256, ctypes.byref(off), ctypes.byref(numel)))
+            self.index[buf.value.decode()] = (off.value, numel.value)
+        dev = self.device
+        self.P = torch.zeros(self.n, dtype=torch.float32, device=dev)
+        self.G = torch.zeros(self.n, dtype=torch.float32, device=dev)
+        self.M = torch.zeros(self.n, dtype=torch.float32, device=dev)
+        self.V = torch.zeros(self.n, dtype=torch.float32, device=dev)
+        self.E = torch.zeros(self.n, dtype=torch.float32, device=dev)
+        self.WB = torch.zeros(self.n, dtype=torch.bfloat16, device=dev)
+        self.WT = torch.zeros(max(nwt.value, 1), dtype=torch.bfloat16, device=dev)
+        _lib.check(self.lib.pdm_train_set_buffers(h, _lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.WB),
+                                                  _lib.ptr(self.WT)), "pdm_train_set_buffers")
+        self.optimizer = dict(name="adamw", lr=2e-4, weight_decay=0.03, betas=(0.99, 0.99), eps=1e-8)
+        self.optimizer.update(optimizer or {})
+        if self.optimizer["name"] != "adamw":
+            raise NotImplementedError(self.optimizer["name"])
+        self.lr_scheduler = dict(name="customized", warmup_steps=-1)
+        self.lr_scheduler.update(lr_scheduler or {})
+        if self.lr_scheduler["name"] != "customized":
+            raise NotImplementedError(self.lr_scheduler["name"])
+        self.ema_rate = ema_rate
+        self.step = 0
+        self.shapes = {}
+        self.ws = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                self.lib.pdm_train_destroy(self.h)
+        except Exception:
+            pass
+
+    # ---- parameters ----------------------------------------------------------------------------------------
+    def _view(self, flat, name):
+        off, numel = self.index[name]
+        return flat[off: off + numel].view(self.shapes.get(name, (numel,)))
+
+    def load_state_dict(self, sd, ema_sd=None):
+        """Reference-keyed state_dict -> parameters (strict), bf16 working copies; the EMA copy starts equal to the
+        parameters (utils.initialize_train_state: ema_update(0)) unless ema_sd is given."""
+        missing = set(self.index) - set(sd)
+        extra = set(sd) - set(self.index)
+        if missing or extra:
+            raise KeyError(f"state_dict mismatch: missing {sorted(missing)[:5]}, unexpected {sorted(extra)[:5]}")
+        with torch.no_grad():
+            for k, v in sd.items():
+                self.shapes[k] = tuple(v.shape)
+                self._view(self.P, k).copy_(v.to(self.device, torch.float32).view(self.shapes[k]))
+            self.E.copy_(self.P)
+            if ema_sd is not None:
+                for k, v in ema_sd.items():
+                    self._view(self.E, k).copy_(v.to(self.device, torch.float32))
+        _lib.check(self.lib.pdm_train_refresh(self.h, _lib.stream_ptr(self.device)), "pdm_train_refresh")
+
+    def state_dict(self):
+        return {k: self._view(self.P, k).clone() for k in self.index}
+
+    def ema_state_dict(self):
+        return {k: self._view(self.E, k).clone() for k in self.index}
+
+    def grads(self):
+        return {k: self._view(self.G, k).clone() for k in self.index}
+
+    # ---- one step --------------------------------------------------------------------------------------------
+    def _workspace(self, rows):
+        need = ctypes.c_size_t()
+        _lib.check(self.lib.pdm_train_workspace_size(self.h, rows, ctypes.byref(need)), "pdm_train_workspace_size")
+        if self.ws is None or self.ws.numel() < need.value:
+            self.ws = None
+            self.ws = torch.empty(need.value, dtype=torch.uint8, device=self.device)
+        return self.ws
+
+    def forward_backward(self, xt, t_in, y, target, gscale=None):
+        """loss[b] = mos(target - nnet(xt, t_in, y)) and d(gscale * sum(loss)) / d(params) into the gradient buffer
+        (gscale default 1/B = loss.mean()).  Returns the per-sample losses."""
+        B = xt.shape[0]
+        xt = xt.to(self.device, torch.float32).contiguous()
+        target = target.to(self.device, torch.float32).contiguous()
+        t_in = t_in.to(self.device, torch.float32).contiguous().reshape(B)
+        if y is not None:
+            y = y.to(self.device, torch.int64).contiguous()
+        loss = torch.empty(B, dtype=torch.float32, device=self.device)
+        ws = self._workspace(B)
+        _lib.check(self.lib.pdm_train_step(self.h, _lib.ptr(xt), _lib.ptr(t_in), _lib.ptr(y), _lib.ptr(target),
+                                           _lib.ptr(loss), B, float(1.0 / B if gscale is None else gscale),
+                                           _lib.ptr(ws), ws.numel(), _lib.stream_ptr(self.device)), "pdm_train_step")
+        return loss
+
+    def all_reduce_grads(self):
+        """DDP: average the gradient buffer over the process group (RCCL on the GPU)."""
+        average_gradients(self.G)
+
+    def optimizer_step(self):
+        """AdamW at the current scheduled LR, then the EMA update; advances the step counter."""
+        o = self.optimizer
+        lr = customized_lr(o["lr"], self.step, self.lr_scheduler.get("warmup_steps", -1))
+        b1, b2 = o["betas"]
+        _lib.check(self.lib.pdm_train_adamw(self.h, _lib.ptr(self.M), _lib.ptr(self.V), _lib.ptr(self.E), float(lr),
+                                            float(b1), float(b2), float(o.get("eps", 1e-8)), float(o["weight_decay"]),
+                                            self.step + 1, float(self.ema_rate), _lib.stream_ptr(self.device)),
+                   "pdm_train_adamw")
+        self.step += 1
+        return lr
+
+    def train_step(self, x0, y=None, objective="discrete", schedule=None, sde=None, rng=None):
+        """One iteration of train_ldm_discrete.py:159-175 (objective 'discrete', Schedule) or train_ldm.py
+        (objective 'sde', VPSDE + noise_pred).  Returns dict(loss=mean loss over the global batch, lr=...)."""
+        if objective == "discrete":
+            schedule = schedule or Schedule(stable_diffusion_beta_schedule())
+            n, eps, xn = schedule.sample(x0, rng)
+            loss = self.forward_backward(xn, n.float(), y, eps)
+        elif objective == "sde":
+            t, eps, xt = LSimple_sde_sample(sde or VPSDE(), x0)
+            loss = self.forward_backward(xt, t * 999, y, eps)
+        else:
+            raise NotImplementedError(objective)
+        self.all_reduce_grads()
+        lr = self.optimizer_step()
+        m = loss.mean()
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(m, op=dist.ReduceOp.SUM)
+            m /= dist.get_world_size()
+        return dict(loss=m, lr=lr)
+
+
+def average_gradients(g):
+    """All-reduce-average a flat gradient tensor over the default process group (no-op at world size 1)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(g, op=dist.ReduceOp.SUM)
+        g /= dist.get_world_size()
+    return g
+
+
+def LSimple_sde_sample(sde, x0, t_init=0):
+    """SDE.sample (sde.py:64-69): t ~ U(t_init, 1), xt = sqrt(cum_alpha(t)) x0 + sqrt(cum_beta(t)) eps."""
+    t = torch.rand(x0.shape[0], device=x0.device) * (1. - t_init) + t_init
+    mean = stp(sde.cum_alpha(t) ** 0.5, x0)
+    std = sde.cum_beta(t) ** 0.5
+    eps = torch.randn_like(x0)
+    return t, eps, mean + stp(std, eps)
+
+
+def LSimple(x0, nnet, schedule, **kwargs):
+    """train_ldm_discrete.py:87-90 on any callable net (e.g. the HIP U-ViT's forward): per-sample losses."""
+    n, eps, xn = schedule.sample(x0)
+    eps_pred = nnet(xn, n, **kwargs)
+    return mos(eps - eps_pred)
+
+
+__all__ = ["Schedule", "stable_diffusion_beta_schedule", "LSimple", "LSimple_sde_sample", "HipTrainState",
+           "drop_labels", "customized_lr", "average_gradients"]

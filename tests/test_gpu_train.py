@@ -1,0 +1,201 @@
+"""GPU parity of the LSimple training step through the C-ABI: each backward kernel against
+fp32 torch autograd, the whole step against the oracle (itself pinned to the reference's training loop,
+tests/test_train_oracle.py) and against the reference's own three-iteration loop (tests/golden/train_golden.npz).
+
+Tolerances (bf16 GEMM operands, fp32 accumulation, as the reference's autocast run): per-kernel outputs rel-L2 <= 1e-2;
+loss <= 1e-2; gradients per tensor rel-L2 <= 3e-2 (tiny nets) / 5e-2 (full U-ViT-L/2 shape); the optimizer in fp32
+(fed the reference's own gradients) within 2 ulp per element."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def tg():
+    return np.load(os.path.join(REPO, "tests", "golden", "train_golden.npz"))
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 192, 320), (33, 64, 16), (66 * 4, 64, 256), (8256, 1024, 4096),
+                                   (8256, 3072, 1024), (517, 16, 1024)])
+def test_wgrad_vs_torch(M, N, K):
+    from panopticdiffusionmodels_amd import _lib
+    g = torch.Generator().manual_seed(M + N + K)
+    dy = torch.randn(M, N, generator=g).bfloat16()
+    x = torch.randn(M, K, generator=g).bfloat16()
+    ref = dy.double().t() @ x.double()
+    out = _lib.wgrad(dy.to(DEV), x.to(DEV))
+    assert rel(out, ref) < 1e-5
+    acc = torch.randn(N, K, generator=g)
+    out2 = _lib.wgrad(dy.to(DEV), x.to(DEV), out=acc.to(DEV).clone(), accumulate=True)
+    assert rel(out2, ref + acc.double()) < 1e-5
+    out3 = _lib.wgrad(dy.to(DEV), x.to(DEV), scratch_mb=0)   # no scratch: one pass over the whole reduction
+    assert rel(out3, ref) < 1e-5
+
+
+@pytest.mark.parametrize("B,L,H", [(2, 66, 1), (2, 258, 2), (3, 17, 2), (1, 288, 3), (2, 257, 1)])
+def test_attention_backward_vs_autograd(B, L, H):
+    from panopticdiffusionmodels_amd import _lib
+    Dh = 64
+    g = torch.Generator().manual_seed(B * 1000 + L + H)
+    qkv = (torch.randn(B * L, 3 * H * Dh, generator=g) * 1.5).bfloat16()
+    dout = torch.randn(B * L, H * Dh, generator=g).bfloat16()
+    q = qkv.float().reshape(B, L, 3, H, Dh).permute(2, 0, 3, 1, 4).clone().requires_grad_(True)
+    att = torch.softmax(q[0] @ q[1].transpose(-1, -2) * Dh ** -0.5, -1) @ q[2]
+    o = att.permute(0, 2, 1, 3).reshape(B * L, H * Dh)
+    o.backward(dout.float())
+    ref = q.grad.permute(1, 3, 0, 2, 4).reshape(B * L, 3 * H * Dh)
+    o_gpu = _lib.attention(qkv.to(DEV), B, L, H, Dh)
+    dq = _lib.attention_backward(qkv.to(DEV), o_gpu, dout.to(DEV), B, L, H, Dh)
+    D = H * Dh
+    for part, sl in (("q", slice(0, D)), ("k", slice(D, 2 * D)), ("v", slice(2 * D, 3 * D))):
+        assert rel(dq[:, sl].float(), ref[:, sl]) < 1e-2, part
+
+
+@pytest.mark.parametrize("rows,D,bf", [(100, 64, True), (517, 1024, True), (300, 1152, False), (7, 512, False)])
+def test_layernorm_backward_vs_autograd(rows, D, bf):
+    from panopticdiffusionmodels_amd import _lib
+    g = torch.Generator().manual_seed(rows + D)
+    x = torch.randn(rows, D, generator=g) * 2 + 0.5
+    gamma = torch.randn(D, generator=g) * 0.2 + 1
+    beta = torch.randn(D, generator=g) * 0.1
+    dh = torch.randn(rows, D, generator=g)
+    if bf:
+        dh = dh.bfloat16()
+    xr = x.clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr, (D,), gr, br, 1e-5).backward(dh.float())
+    acc = torch.randn(rows, D, generator=g)
+    dx, dxb, dgm, dbt = _lib.layernorm_backward(x.to(DEV), dh.to(DEV), gamma.to(DEV), dx=acc.to(DEV).clone(),
+                                                accumulate=True)
+    assert rel(dx, xr.grad + acc) < 1e-5
+    assert rel(dxb.float(), xr.grad + acc) < 5e-3
+    assert rel(dgm, gr.grad) < 1e-5 and rel(dbt, br.grad) < 1e-5
+
+
+def _state(name, seed=11, init="random"):
+    from panopticdiffusionmodels_amd import configs, weights
+    from panopticdiffusionmodels_amd.train import HipTrainState
+    full = configs.get_config(name)
+    sd = weights.nnet_state_dict(full["nnet"], seed=seed, init=init)
+    st = HipTrainState(full["nnet"], DEV, optimizer=full.get("optimizer"), lr_scheduler=full.get("lr_scheduler"),
+                       ema_rate=full.get("train", {}).get("ema_rate", 0.9999))
+    st.load_state_dict(sd)
+    kw = dict(full["nnet"])
+    kw.pop("name")
+    return full, kw, sd, st
+
+
+@pytest.mark.parametrize("name", ["tiny_uvit_train", "tiny_uvit_train_uncond"])
+def test_train_step_grads_vs_reference(name, tg):
+    """First iteration of the reference's loop: per-sample loss and every parameter's gradient."""
+    full, kw, sd, st = _state(name)
+    y = torch.from_numpy(tg[f"{name}/y"]) if f"{name}/y" in tg.files else None
+    loss = st.forward_backward(torch.from_numpy(tg[f"{name}/it0_xt"]), torch.from_numpy(tg[f"{name}/it0_t"]), y,
+                               torch.from_numpy(tg[f"{name}/it0_eps"]))
+    assert rel(loss, tg[f"{name}/it0_loss"]) < 1e-2
+    grads = st.grads()
+    bad = {k: rel(grads[k], tg[f"{name}/grad/{k}"]) for k in grads}
+    worst = max(bad.values())
+    assert worst < 3e-2, sorted(bad.items(), key=lambda kv: -kv[1])[:5]
+
+
+@pytest.mark.parametrize("name", ["tiny_uvit_train", "tiny_uvit_train_uncond"])
+def test_adamw_ema_vs_reference(name, tg):
+    """The optimizer + EMA kernel fed the reference's own first-iteration gradients: parameters after one AdamW
+    step at lr 2e-4 (and the EMA) against torch.optim.AdamW semantics (oracle.train_ref.adamw_step)."""
+    from oracle import train_ref
+    full, kw, sd, st = _state(name)
+    opt = full["optimizer"]
+    g = {k: torch.from_numpy(tg[f"{name}/grad/{k}"]) for k in sd}
+    with torch.no_grad():
+        for k, v in g.items():
+            st._view(st.G, k).copy_(v.to(DEV).view(st._view(st.G, k).shape))
+    st.lr_scheduler["warmup_steps"] = -1
+    st.optimizer_step()
+    p, e = st.state_dict(), st.ema_state_dict()
+    for k in sd:
+        pr, _, _ = train_ref.adamw_step(sd[k].float(), g[k], torch.zeros_like(g[k]), torch.zeros_like(g[k]), 1,
+                                        opt["lr"], opt["betas"], 1e-8, opt["weight_decay"])
+        er = train_ref.ema(sd[k].float(), pr, full["train"]["ema_rate"])
+        # fp32 update of both: within 2 ulp of each element (the displacement itself is ~1e-3 of a parameter)
+        assert bool(((p[k].cpu() - pr).abs() <= 2.5e-7 * pr.abs() + 1e-9).all()), k
+        assert bool(((e[k].cpu() - er).abs() <= 2.5e-7 * er.abs() + 1e-9).all()), k
+    # the bf16 working copy follows the parameters
+    off, n = st.index["mid_block.mlp.fc1.weight"]
+    assert torch.equal(st.WB[off:off + n], st.P[off:off + n].bfloat16())
+
+
+@pytest.mark.parametrize("name", ["tiny_uvit_train", "tiny_uvit_train_uncond"])
+def test_three_iterations_vs_reference(name, tg):
+    """The reference's three-iteration loop (warm-up LR 0, 0.2 lr, 0.4 lr; EMA): losses per iteration and the final
+    parameters' displacement from the initial ones."""
+    full, kw, sd, st = _state(name)
+    y = torch.from_numpy(tg[f"{name}/y"]) if f"{name}/y" in tg.files else None
+    for i in range(3):
+        loss = st.forward_backward(torch.from_numpy(tg[f"{name}/it{i}_xt"]), torch.from_numpy(tg[f"{name}/it{i}_t"]),
+                                   y, torch.from_numpy(tg[f"{name}/it{i}_eps"]))
+        assert rel(loss, tg[f"{name}/it{i}_loss"]) < 1e-2, i
+        lr = st.optimizer_step()
+        assert abs(lr - float(tg[f"{name}/it{i}_lr"])) < 1e-12
+    p, e = st.state_dict(), st.ema_state_dict()
+    num = den = 0.0
+    for k in sd:
+        d_ref = torch.from_numpy(tg[f"{name}/param/{k}"]).double() - sd[k].double()
+        d = p[k].cpu().double() - sd[k].double()
+        num += float((d - d_ref).norm() ** 2)
+        den += float(d_ref.norm() ** 2)
+        assert rel(e[k], tg[f"{name}/ema/{k}"]) < 1e-3, k
+    # Adam normalises each element's step, so elements whose gradient is near zero move by a bf16-noise-driven
+    # amount; the displacement as a whole must still follow the reference's
+    assert (num / den) ** 0.5 < 0.25, (num / den) ** 0.5
+
+
+def test_train_step_full_L2_shape_vs_oracle():
+    """U-ViT-L/2 at full width / depth / token count (D 1024, 21 blocks, L 258), 2 images: loss and gradients vs the
+    oracle's fp32 autograd."""
+    from oracle import train_ref
+    full, kw, sd, st = _state("imagenet256_uvit_large", seed=3, init="random")
+    g = torch.Generator().manual_seed(8)
+    B = 2
+    xt = torch.randn(B, 4, 32, 32, generator=g)
+    t = torch.rand(B, generator=g) * 999
+    y = torch.tensor([5, 1000])
+    eps = torch.randn(B, 4, 32, 32, generator=g)
+    loss = st.forward_backward(xt, t, y, eps)
+    lref, gref = train_ref.lsimple_grads(sd, kw, xt, t, y, eps)
+    assert rel(loss, lref) < 1e-2
+    grads = st.grads()
+    bad = {k: rel(grads[k], gref[k]) for k in grads if float(gref[k].norm()) > 0}
+    worst = max(bad.values())
+    assert worst < 5e-2, sorted(bad.items(), key=lambda kv: -kv[1])[:5]
+
+
+def test_train_step_batch_invariance():
+    """Per-sample losses do not depend on the batch they are computed in; gradients of a duplicated batch equal those
+    of the single copy (gscale = 1 / B)."""
+    full, kw, sd, st = _state("tiny_uvit_train")
+    g = torch.Generator().manual_seed(2)
+    xt = torch.randn(3, 4, 16, 16, generator=g)
+    t = torch.rand(3, generator=g) * 999
+    y = torch.tensor([1, 4, 10])
+    eps = torch.randn(3, 4, 16, 16, generator=g)
+    l1 = st.forward_backward(xt, t, y, eps).cpu()
+    g1 = {k: v.cpu() for k, v in st.grads().items()}
+    l2 = st.forward_backward(torch.cat([xt, xt]), torch.cat([t, t]), torch.cat([y, y]), torch.cat([eps, eps])).cpu()
+    g2 = st.grads()
+    assert torch.allclose(l2[:3], l1, rtol=1e-5, atol=1e-7) and torch.allclose(l2[3:], l1, rtol=1e-5, atol=1e-7)
+    for k in g1:
+        assert rel(g2[k], g1[k]) < 1e-3 or float(g1[k].norm()) == 0, k

@@ -1,0 +1,152 @@
+"""CPU checks of the training step: the oracle (oracle/train_ref.py) against the reference's own
+training loop (tests/golden/train_golden.npz, tests/golden/make_train_golden.py), the host-side noise draws / LR
+schedule of panopticdiffusionmodels_amd.train against the same fixtures, and the pdm_train parameter table (pure host
+logic, no GPU call) against the reference state_dict keys."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import train_ref
+from panopticdiffusionmodels_amd import configs, weights
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NAMES = ["tiny_uvit_train", "tiny_uvit_train_uncond"]
+
+
+@pytest.fixture(scope="module")
+def tg():
+    return np.load(os.path.join(REPO, "tests", "golden", "train_golden.npz"))
+
+
+def rel(a, b):
+    a, b = torch.as_tensor(a).double(), torch.as_tensor(b).double()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def _setup(name, tg):
+    full = configs.get_config(name)
+    cfg = full["nnet"]
+    sd = weights.nnet_state_dict(cfg, seed=11, init="random")
+    kw = dict(cfg)
+    kw.pop("name")
+    x0 = torch.from_numpy(tg[f"{name}/x0"])
+    y = torch.from_numpy(tg[f"{name}/y"]) if f"{name}/y" in tg.files else None
+    return full, kw, sd, x0, y
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_noise_draws_match_reference(name, tg):
+    """Schedule.sample / VPSDE sample restated (oracle and product host code) reproduce the reference's draws."""
+    from panopticdiffusionmodels_amd import train
+    full, kw, sd, x0, y = _setup(name, tg)
+    for i in range(3):
+        nps, ts = 100 + i, 200 + i
+        if full["train"]["objective"] == "discrete":
+            n, eps, xt = train_ref.discrete_sample(x0, nps, ts)
+            t_in = n.float()
+            np.random.seed(nps)
+            torch.manual_seed(ts)
+            n2, eps2, xt2 = train.Schedule(train.stable_diffusion_beta_schedule()).sample(x0)
+            assert torch.equal(n2.float(), t_in) and torch.equal(eps2, eps)
+            assert rel(xt2, xt) < 1e-6
+        else:
+            t, eps, xt = train_ref.sde_sample(x0, ts)
+            t_in = t * 999
+            torch.manual_seed(ts)
+            t2, eps2, xt2 = train.LSimple_sde_sample(train.VPSDE(), x0)
+            assert torch.equal(t2, t) and torch.equal(eps2, eps)
+            assert rel(xt2, xt) < 1e-6
+        assert rel(t_in, tg[f"{name}/it{i}_t"]) < 1e-7
+        assert torch.equal(eps, torch.from_numpy(tg[f"{name}/it{i}_eps"]))
+        assert rel(xt, tg[f"{name}/it{i}_xt"]) < 1e-6
+        opt = full["optimizer"]
+        lr = train.customized_lr(opt["lr"], i, full["lr_scheduler"]["warmup_steps"])
+        assert abs(lr - float(tg[f"{name}/it{i}_lr"])) <= 1e-12
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_training_loop_vs_reference(name, tg):
+    """Three reference train_step iterations: losses, first-iteration gradients, final parameters and EMA."""
+    full, kw, sd, x0, y = _setup(name, tg)
+    draws = [(100 + i, 200 + i) for i in range(3)]
+    losses, g0, p, e = train_ref.train_steps(sd, kw, x0, y, draws, full["train"]["objective"], full["optimizer"],
+                                             full["lr_scheduler"]["warmup_steps"], full["train"]["ema_rate"])
+    for i in range(3):
+        assert rel(losses[i], tg[f"{name}/it{i}_loss"]) < 1e-5, i
+    worst = max(rel(g0[k], tg[f"{name}/grad/{k}"]) for k in sd if float(np.abs(tg[f"{name}/grad/{k}"]).sum()) > 0)
+    assert worst < 1e-4, worst
+    for k in sd:
+        d_ref = torch.from_numpy(tg[f"{name}/param/{k}"]).double() - sd[k].double()
+        d = p[k].double() - sd[k].double()
+        assert float((d - d_ref).norm()) <= 1e-3 * float(d_ref.norm()) + 1e-7, k
+        assert rel(e[k], tg[f"{name}/ema/{k}"]) < 1e-6, k
+
+
+def test_train_param_table_without_gpu():
+    """pdm_train_create's flat parameter table covers exactly the reference state_dict keys with their sizes, 64-element
+    aligned, in backward order (head first, embeddings last)."""
+    from panopticdiffusionmodels_amd import _lib, native
+    lib = _lib.load()
+    for name in ["imagenet256_uvit_large", "cifar10_uvit_small", "tiny_uvit_train", "tiny_uvit_train_uncond"]:
+        kw = configs.nnet_kwargs(name)
+        kw.pop("name")
+        h = ctypes.c_void_p()
+        _lib.check(lib.pdm_train_create(ctypes.byref(native.cfg_struct(kw, False)), ctypes.byref(h)))
+        spec = {k: int(np.prod(s)) for k, s, _ in weights.uvit_spec(**kw)}
+        buf = ctypes.create_string_buffer(256)
+        seen, offs = {}, []
+        for i in range(lib.pdm_train_param_count(h)):
+            off, ne = ctypes.c_longlong(), ctypes.c_longlong()
+            _lib.check(lib.pdm_train_param_info(h, i, buf, 256, ctypes.byref(off), ctypes.byref(ne)))
+            seen[buf.value.decode()] = ne.value
+            offs.append(off.value)
+            assert off.value % 64 == 0
+        assert seen == spec, name
+        assert offs == sorted(offs)
+        keys = list(seen)
+        assert keys[-1] == "patch_embed.proj.bias" and "decoder_pred.weight" in keys[:4]
+        n, nwt = ctypes.c_longlong(), ctypes.c_longlong()
+        _lib.check(lib.pdm_train_sizes(h, ctypes.byref(n), ctypes.byref(nwt)))
+        assert n.value >= sum(spec.values())
+        ws = ctypes.c_size_t()
+        _lib.check(lib.pdm_train_workspace_size(h, 4, ctypes.byref(ws)))
+        assert ws.value > 0
+        with pytest.raises(RuntimeError):   # no buffers registered: a state error, no GPU call
+            _lib.check(lib.pdm_train_refresh(h, None))
+        lib.pdm_train_destroy(h)
+    # unsupported nets are rejected up front
+    kw = configs.nnet_kwargs("tiny_uvit_cond")   # head dim 32
+    kw.pop("name")
+    h = ctypes.c_void_p()
+    with pytest.raises(ValueError):
+        _lib.check(lib.pdm_train_create(ctypes.byref(native.cfg_struct(kw, False)), ctypes.byref(h)))
+
+
+def test_gradient_average_gloo():
+    """average_gradients (the DDP step between backward and AdamW) over a world-2 gloo group."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + os.getpid() % 200
+    ps = [ctx.Process(target=_avg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for r, v in out:
+        assert np.allclose(v, np.arange(6, dtype=np.float32) * 1.5), (r, v)
+
+
+def _avg_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from panopticdiffusionmodels_amd.train import average_gradients
+    g = torch.arange(6, dtype=torch.float32) * (rank + 1)
+    average_gradients(g)
+    q.put((rank, g.numpy()))
+    dist.destroy_process_group()

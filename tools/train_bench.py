@@ -1,0 +1,97 @@
+"""Throughput of the HIP LSimple training step on one GPU.
+
+    python tools/train_bench.py [--config imagenet256_uvit_large] [--batch 64] [--steps 5] [--warmup 2]
+
+One step = the reference's train_step (train_ldm_discrete.py:159-175 / train_ldm.py): noise draw, forward with
+saved activations, LSimple loss, backward, AdamW + EMA, on a fixed synthetic latent batch (seeded random-init
+weights).  Prints one JSON line: images/s, ms per step split into forward+backward and optimizer (HIP events on the
+launch stream), and the algorithmic rate: 3 x the forward's GEMM + attention FLOPs per image (dX and dW GEMMs each
+cost one forward GEMM; the attention backward recomputes the scores: 7 / 2 of the forward's attention FLOPs are
+counted as 2 + ... only the textbook 2.5x is counted).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from panopticdiffusionmodels_amd import configs, weights  # noqa: E402
+from panopticdiffusionmodels_amd.train import HipTrainState, Schedule, stable_diffusion_beta_schedule  # noqa: E402
+
+
+def train_flops_per_image(cfg):
+    D, depth = cfg["embed_dim"], cfg["depth"]
+    Hd = int(D * cfg.get("mlp_ratio", 4))
+    L = (cfg["img_size"] // cfg["patch_size"]) ** 2 + (2 if cfg.get("num_classes", -1) > 0 else 1)
+    nb = 2 * (depth // 2) + 1
+    gemm = nb * 2 * L * (3 * D * D + D * D + 2 * D * Hd) + (depth // 2) * 2 * L * 2 * D * D
+    attn = nb * 4 * L * L * D
+    return 3 * gemm + 2.5 * attn   # fwd + dX + dW GEMMs; attention fwd + the 1.5x backward (dS, dQ/dK/dV)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="imagenet256_uvit_large")
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    args = ap.parse_args()
+    full = configs.get_config(args.config)
+    dev = torch.device("cuda")
+    sd = weights.nnet_state_dict(full["nnet"], seed=0, init="reference")
+    st = HipTrainState(full["nnet"], dev, optimizer=full.get("optimizer"), lr_scheduler=full.get("lr_scheduler"),
+                       ema_rate=full.get("train", {}).get("ema_rate", 0.9999))
+    st.load_state_dict(sd)
+    del sd
+    g = torch.Generator().manual_seed(0)
+    B = args.batch
+    x0 = torch.randn(B, *full["z_shape"], generator=g).to(dev)
+    ncls = full["nnet"].get("num_classes", -1)
+    y = torch.randint(0, ncls, (B,), generator=g).to(dev) if ncls > 0 else None
+    sched = Schedule(stable_diffusion_beta_schedule())
+    import numpy as np
+    rng = np.random.RandomState(0)
+
+    def step(timed):
+        n, eps, xn = sched.sample(x0, rng)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed else None
+        if timed:
+            e[0].record()
+        loss = st.forward_backward(xn, n.float(), y, eps)
+        if timed:
+            e[1].record()
+        st.optimizer_step()
+        if timed:
+            e[2].record()
+        return loss, e
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    evs = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss, e = step(True)
+        evs.append(e)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    fb = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)
+    opt = sum(e[1].elapsed_time(e[2]) for e in evs) / len(evs)
+    fl = train_flops_per_image(full["nnet"])
+    ips = B / dt
+    print(json.dumps({
+        "metric": f"training images/s, {args.config} LSimple step (fwd + bwd + AdamW + EMA), 1 GPU",
+        "value": round(ips, 2), "unit": "images/sec", "batch": B, "steps": args.steps, "ms_per_step": round(dt * 1e3, 2),
+        "fwd_bwd_ms": round(fb, 2), "adamw_ema_ms": round(opt, 2), "params": sum(v[1] for v in st.index.values()),
+        "algorithmic_tflop_per_image": round(fl / 1e12, 4), "achieved_tflops": round(ips * fl / 1e12, 1),
+        "frac_of_bf16_peak": round(ips * fl / 2.5e15, 4), "loss": float(loss.mean()),
+        "workspace_gb": round(st.ws.numel() / 1e9, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
