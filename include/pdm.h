@@ -329,6 +329,8 @@ int pdm_train_adamw(pdm_trainer* t, float* m, float* v, float* ema, float lr, fl
  * pdm_layernorm_backward: nn.LayerNorm(D) over fp32 rows x, dh the output gradient (fp32, or bf16 if dh_bf16) ->
  * dx (+= if accumulate), optional bf16 copy dxb, dgamma, dbeta (written); scratch >= (4 ceil(rows/4) + 1) 8 D bytes
  * is plenty. */
+/* dW tile policy (0 = automatic: 256 x 128 for n >= 256, else 128 x 128; 128 / 256 force one, A/B timing) */
+int pdm_set_wgrad_tile(int tile);
 int pdm_wgrad(const void* A, int lda, const void* B, int ldb, float* C, int ldc, int M, int N, int K, int accumulate,
               float* scratch, size_t scratch_bytes, void* stream);
 int pdm_attention_backward(const void* qkv, const void* o, const void* dout, void* dqkv, int B, int L, int H, int Dh,

@@ -20,6 +20,7 @@ struct WgradArgs {
   int accumulate;
 };
 const char* wgrad_check(const WgradArgs& p);
+extern int g_wgrad_tile;   // 0 = automatic tile, 128 / 256 = forced n-tile (timing A/B)
 hipError_t wgrad_launch(const WgradArgs& p, float* part, size_t part_bytes, hipStream_t stream);
 
 // dst[c] (+)= sum_r x[gather(r)][c] over `rows` rows of `ncols` columns (bias / pos_embed gradients)

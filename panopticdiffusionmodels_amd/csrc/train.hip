@@ -553,6 +553,12 @@ int pdm_train_adamw(pdm_trainer* t, float* m, float* v, float* ema, float lr, fl
   return refresh(t, s);
 }
 
+int pdm_set_wgrad_tile(int tile) {
+  if (tile != 0 && tile != 128 && tile != 256) return pdm::set_error(PDM_ERR_ARG, "pdm_set_wgrad_tile: 0, 128 or 256");
+  pdm::g_wgrad_tile = tile;
+  return PDM_OK;
+}
+
 // ---- individual training kernels (parity tests) ----
 int pdm_wgrad(const void* A, int lda, const void* B, int ldb, float* C, int ldc, int M, int N, int K, int accumulate,
               float* scratch, size_t scratch_bytes, void* stream) {

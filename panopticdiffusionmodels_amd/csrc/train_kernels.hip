@@ -54,20 +54,25 @@ int grid_for(long long n, int per_block = 256) {
 
 // ------------------------------------------------------------------------------------------------
 // dW[n][k] (+)= sum_m A[m][n] B[m][k]
-// Tile 128 (n) x 128 (k), 4 waves (2 x 2, 64 x 64 each = 4 x 4 mfma_f32_16x16x32_bf16 accumulators), reduction
-// stages of 32 rows.  A stage of one operand is 32 rows x 256 B = 8 LDS-DMA pieces of 1 KiB (4 rows each); the
-// 16-byte chunk c of row r is stored at chunk c ^ swz(r) so that the transposed fragment reads (per 32-lane half:
-// rows g*8 + q, q < 4, of both 16-lane groups, two chunks each) touch all 64 banks once.  3-slot ring.
+// Tile TN (n) x 128 (k), 4 waves, reduction stages of 32 rows, 3-slot LDS ring filled by LDS-DMA.
+//   TN = 128: waves 2 x 2, 64 x 64 each (4 x 4 mfma_f32_16x16x32_bf16 accumulators)
+//   TN = 256: waves 4 x 1, 64 x 128 each (8 x 4 accumulators: 12 fragments per 32 MFMAs instead of 8 per 16)
+// A stage of an operand is 32 rows of TN (A) / 128 (B) columns; 1-KiB LDS-DMA pieces hold 1024 / (2 cols) rows.  The
+// 16-byte chunk c of row r is stored at chunk c ^ swz(r) so that a transposed fragment read (per 32-lane half: rows
+// g*8 + q, q < 4, of both 16-lane groups, two chunks each) touches all 64 banks once, for 256- and 512-byte rows alike.
 __device__ __forceinline__ int wg_swz(int r) { return ((((r >> 3) & 1) << 2) | (r & 3)) << 1; }
 
+template <int TN>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p, int tiles_k) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TB = 32 * 256;
-  constexpr int SB = 2 * TB;
+  constexpr int TA = 32 * TN * 2, TB = 32 * 128 * 2, SB = TA + TB;
+  constexpr int APW = TA / 1024 / 4, BPW = TB / 1024 / 4;     // LDS-DMA pieces per wave and stage
+  constexpr int ARB = TN * 2, BRB = 256;                        // row bytes
+  constexpr int NI = 4, KI = TN == 256 ? 8 : 4;                 // fragments per wave along n / k
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wn = wave >> 1, wk = wave & 1;
+  const int wn = TN == 256 ? wave : wave >> 1, wk = TN == 256 ? 0 : wave & 1;
   const int tn = blockIdx.x / tiles_k, tk = blockIdx.x - tn * tiles_k;
-  const int n0 = tn * 128, k0 = tk * 128;
+  const int n0 = tn * TN, k0 = tk * 128;
   const int ms = blockIdx.y * p.mchunk;
   const int me = min(p.M, ms + p.mchunk);
   const int nk = (me - ms + 31) >> 5;
@@ -78,71 +83,79 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p, int tiles_k)
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, arows * p.lda * 2);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, brows * p.ldb * 2);
 
-  const int prow = lane >> 4, pch = lane & 15;
-  int rr[2];
-  unsigned ac[2], bc[2];
+  // per-lane row (within the stage) and column byte offset of this wave's pieces
+  int ar[APW], br[BPW];
+  unsigned ac[APW], bc[BPW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    rr[i] = (wave * 2 + i) * 4 + prow;
-    const int sw = (pch ^ wg_swz(rr[i])) * 8;   // logical column chunk loaded into physical chunk pch
-    ac[i] = (unsigned)(n0 + sw) * 2u;
-    bc[i] = (unsigned)(k0 + sw) * 2u;
+  for (int i = 0; i < APW; ++i) {
+    constexpr int rows_pp = 1024 / ARB, cpr = ARB / 16;
+    ar[i] = (wave * APW + i) * rows_pp + lane / cpr;
+    ac[i] = (unsigned)(n0 + (((lane % cpr) ^ wg_swz(ar[i])) * 8)) * 2u;
+  }
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) {
+    br[i] = (wave * BPW + i) * 4 + (lane >> 4);
+    bc[i] = (unsigned)(k0 + (((lane & 15) ^ wg_swz(br[i])) * 8)) * 2u;
   }
   auto issue = [&](int kt, int buf) {
     char* sa = smem + buf * SB;
-    char* sb = sa + TB;
+    char* sb = sa + TA;
+    const int mb = ms + kt * 32;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = ms + kt * 32 + rr[i];
-      unsigned oa = OOB, ob = OOB;
-      if (m < me) {
-        oa = (unsigned)gather_row(m, p.a_rpg, p.a_gs, p.a_off) * (unsigned)(p.lda * 2) + ac[i];
-        ob = (unsigned)gather_row(m, p.b_rpg, p.b_gs, p.b_off) * (unsigned)(p.ldb * 2) + bc[i];
-      }
-      dma16(ra, oa, (PDM_LDS void*)(sa + (wave * 2 + i) * 1024));
-      dma16(rb, ob, (PDM_LDS void*)(sb + (wave * 2 + i) * 1024));
+    for (int i = 0; i < APW; ++i) {
+      const int m = mb + ar[i];
+      const unsigned o = m < me ? (unsigned)gather_row(m, p.a_rpg, p.a_gs, p.a_off) * (unsigned)(p.lda * 2) + ac[i] : OOB;
+      dma16(ra, o, (PDM_LDS void*)(sa + (wave * APW + i) * 1024));
+    }
+#pragma unroll
+    for (int i = 0; i < BPW; ++i) {
+      const int m = mb + br[i];
+      const unsigned o = m < me ? (unsigned)gather_row(m, p.b_rpg, p.b_gs, p.b_off) * (unsigned)(p.ldb * 2) + bc[i] : OOB;
+      dma16(rb, o, (PDM_LDS void*)(sb + (wave * BPW + i) * 1024));
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[KI][NI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < KI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
   const int r1 = g * 8 + qq, r2 = r1 + 4;
-  const int o1 = r1 * 256 + (pp & 1) * 8, o2 = r2 * 256 + (pp & 1) * 8;
   const int s1 = wg_swz(r1), s2 = wg_swz(r2);
   if (nk > 0) issue(0, 0);
   if (nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(APW + BPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);
     const char* sa = smem + (kt % 3) * SB;
-    const char* sb = sa + TB;
-    bf16x8 af[4], bfr[4];
+    const char* sb = sa + TA;
+    bf16x8 af[NI], bfr[KI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int ca = ((wn * 64 + i * 16) >> 3) + (pp >> 1);
-      af[i] = tr_frag(sa + o1 + ((ca ^ s1) << 4), sa + o2 + ((ca ^ s2) << 4));
-      const int cb = ((wk * 64 + i * 16) >> 3) + (pp >> 1);
-      bfr[i] = tr_frag(sb + o1 + ((cb ^ s1) << 4), sb + o2 + ((cb ^ s2) << 4));
+      af[i] = tr_frag(sa + r1 * ARB + ((ca ^ s1) << 4) + (pp & 1) * 8, sa + r2 * ARB + ((ca ^ s2) << 4) + (pp & 1) * 8);
     }
 #pragma unroll
-    for (int ki = 0; ki < 4; ++ki)
+    for (int i = 0; i < KI; ++i) {
+      const int cb = ((wk * 64 + i * 16) >> 3) + (pp >> 1);
+      bfr[i] = tr_frag(sb + r1 * BRB + ((cb ^ s1) << 4) + (pp & 1) * 8, sb + r2 * BRB + ((cb ^ s2) << 4) + (pp & 1) * 8);
+    }
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) acc[ki][ni] = mfma16x16x32(bfr[ki], af[ni], acc[ki][ni]);
+    for (int ki = 0; ki < KI; ++ki)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) acc[ki][ni] = mfma16x16x32(bfr[ki], af[ni], acc[ki][ni]);
   }
   // lane: column n = .. + (lane & 15), 4 consecutive k = .. + (lane >> 4) * 4
 #pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
+  for (int ni = 0; ni < NI; ++ni) {
     const int n = n0 + wn * 64 + ni * 16 + i16;
     if (n >= p.N) continue;
 #pragma unroll
-    for (int ki = 0; ki < 4; ++ki) {
+    for (int ki = 0; ki < KI; ++ki) {
       const int k = k0 + wk * 64 + ki * 16 + g * 4;
       if (k >= p.K) continue;
       f32x4* dst = reinterpret_cast<f32x4*>(C + (size_t)n * p.ldc + k);
@@ -702,10 +715,13 @@ const char* wgrad_check(const WgradArgs& p) {
   return nullptr;
 }
 
+int g_wgrad_tile = 0;   // 0 auto, 128 / 256 forced (pdm_set_wgrad_tile, A/B timing)
+
 hipError_t wgrad_launch(const WgradArgs& args, float* part, size_t part_bytes, hipStream_t stream) {
-  constexpr int SMEM = 3 * 2 * 32 * 256;
   WgradArgs p = args;
-  const int tiles_n = (p.N + 127) / 128, tiles_k = (p.K + 127) / 128;
+  // the 256 x 128 tile wherever the n extent fills it (every U-ViT Linear), the 128 x 128 one for narrow outputs
+  const int TN = g_wgrad_tile ? g_wgrad_tile : (p.N >= 256 ? 256 : 128);
+  const int tiles_n = (p.N + TN - 1) / TN, tiles_k = (p.K + 127) / 128;
   const int tiles = tiles_n * tiles_k;
   // split the reduction so that >= ~1024 workgroups run (2 per CU is the residency), >= 512 rows each, and the
   // fp32 partials fit the scratch
@@ -726,7 +742,11 @@ hipError_t wgrad_launch(const WgradArgs& args, float* part, size_t part_bytes, h
   } else {
     p.sC = 0;
   }
-  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, split), dim3(256), SMEM, stream, p, tiles_k);
+  if (TN == 256)
+    hipLaunchKernelGGL(wgrad_kernel<256>, dim3(tiles, split), dim3(256), 3 * (32 * 256 * 2 + 32 * 128 * 2), stream, p,
+                       tiles_k);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<128>, dim3(tiles, split), dim3(256), 3 * (32 * 128 * 2 * 2), stream, p, tiles_k);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || split == 1) return e;
   hipLaunchKernelGGL(reduce_parts_kernel, dim3(grid_for(nk / 4)), dim3(256), 0, stream, part, split, p.N, p.K, args.C,

@@ -27,10 +27,12 @@ def tg():
     return np.load(os.path.join(REPO, "tests", "golden", "train_golden.npz"))
 
 
+@pytest.mark.parametrize("tile", [0, 128, 256])
 @pytest.mark.parametrize("M,N,K", [(1000, 192, 320), (33, 64, 16), (66 * 4, 64, 256), (8256, 1024, 4096),
-                                   (8256, 3072, 1024), (517, 16, 1024)])
-def test_wgrad_vs_torch(M, N, K):
+                                   (8256, 3072, 1024), (517, 16, 1024), (300, 520, 136)])
+def test_wgrad_vs_torch(M, N, K, tile):
     from panopticdiffusionmodels_amd import _lib
+    _lib.check(_lib.load().pdm_set_wgrad_tile(tile))
     g = torch.Generator().manual_seed(M + N + K)
     dy = torch.randn(M, N, generator=g).bfloat16()
     x = torch.randn(M, K, generator=g).bfloat16()
@@ -41,6 +43,7 @@ def test_wgrad_vs_torch(M, N, K):
     out2 = _lib.wgrad(dy.to(DEV), x.to(DEV), out=acc.to(DEV).clone(), accumulate=True)
     assert rel(out2, ref + acc.double()) < 1e-5
     out3 = _lib.wgrad(dy.to(DEV), x.to(DEV), scratch_mb=0)   # no scratch: one pass over the whole reduction
+    _lib.check(_lib.load().pdm_set_wgrad_tile(0))
     assert rel(out3, ref) < 1e-5
 
 
