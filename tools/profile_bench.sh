@@ -7,7 +7,7 @@
 set -e
 TAG=${1:-r03}
 CONFIG=${2:-imagenet256_uvit_large}
-BATCH=${3:-95}
+BATCH=${3:-50}
 PREC=${4:-}
 ROWS=$((2 * BATCH))
 OUT=${GRAFT_REPO_ROOT:-.}/gpurun_out/prof_${TAG}_${CONFIG}
@@ -21,3 +21,10 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-forma
 echo "fetch pass done"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 tools/time_forward.py $CONFIG $ROWS 2 ${PREC:-bf16} > $OUT/write.log 2>&1
 echo "write pass done"
+# summarise on the box (raw traces can exceed gpurun's 64 MiB copy-back), keep the summaries + logs only
+SUM=${GRAFT_REPO_ROOT:-.}/gpurun_out/prof_summaries
+mkdir -p $SUM
+PDM_PROF_DST=$SUM python3 tools/summarize_prof.py $TAG $CONFIG $BATCH ${PREC:-bf16} > /dev/null
+cp $OUT/bench_kt.log $SUM/${TAG}_${CONFIG}_bench_kt.log
+rm -rf $OUT
+echo "summarised into $SUM"

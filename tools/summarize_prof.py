@@ -40,7 +40,7 @@ def main():
     batch = int(sys.argv[3]) if len(sys.argv) > 3 else 95
     precision = sys.argv[4] if len(sys.argv) > 4 else "bf16"
     src = os.path.join(REPO, "gpurun_out", f"prof_{tag}_{config}")
-    dst = os.path.join(REPO, "profiles")
+    dst = os.environ.get("PDM_PROF_DST") or os.path.join(REPO, "profiles")   # on the GPU box: a gpurun_out dir
     os.makedirs(dst, exist_ok=True)
     kt = os.path.join(src, "kt", "run_kernel_stats.csv")
     if os.path.exists(kt):

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--wgrad-tile", type=int, default=0, help="dW GEMM n-tile: 0 auto, 128, 256 (A/B timing)")
+    ap.add_argument("--lanes", type=int, default=2, help="concurrent half-batch lanes (HipTrainState lanes)")
     args = ap.parse_args()
     from panopticdiffusionmodels_amd import _lib
     _lib.check(_lib.load().pdm_set_wgrad_tile(args.wgrad_tile))
@@ -48,7 +49,7 @@ def main():
     dev = torch.device("cuda")
     sd = weights.nnet_state_dict(full["nnet"], seed=0, init="reference")
     st = HipTrainState(full["nnet"], dev, optimizer=full.get("optimizer"), lr_scheduler=full.get("lr_scheduler"),
-                       ema_rate=full.get("train", {}).get("ema_rate", 0.9999))
+                       ema_rate=full.get("train", {}).get("ema_rate", 0.9999), lanes=args.lanes)
     st.load_state_dict(sd)
     del sd
     g = torch.Generator().manual_seed(0)
@@ -93,7 +94,8 @@ def main():
         "fwd_bwd_ms": round(fb, 2), "adamw_ema_ms": round(opt, 2), "params": sum(v[1] for v in st.index.values()),
         "algorithmic_tflop_per_image": round(fl / 1e12, 4), "achieved_tflops": round(ips * fl / 1e12, 1),
         "frac_of_bf16_peak": round(ips * fl / 2.5e15, 4), "loss": float(loss.mean()),
-        "workspace_gb": round(st.ws.numel() / 1e9, 2), "wgrad_tile": args.wgrad_tile or "auto"}), flush=True)
+        "workspace_gb": round(st.ws.numel() / 1e9, 2), "wgrad_tile": args.wgrad_tile or "auto",
+        "lanes": st.lanes}), flush=True)
 
 
 if __name__ == "__main__":
