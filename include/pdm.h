@@ -319,10 +319,11 @@ int pdm_train_workspace_size(const pdm_trainer* t, int rows, size_t* bytes);
  * its activations in the workspace (bf16 GEMM operands, fp32 residual stream). */
 int pdm_train_step(pdm_trainer* t, const float* xt, const float* tvals, const int64_t* y, const float* target,
                    float* loss, int rows, float gscale, void* workspace, size_t workspace_bytes, void* stream);
-/* torch.optim.AdamW step `step` (>= 1, bias corrections 1 - beta^step) over every parameter with the gradient buffer,
- * then ema = ema_rate * ema + (1 - ema_rate) * params (utils.ema; ema may be NULL) and the bf16 copies */
-int pdm_train_adamw(pdm_trainer* t, float* m, float* v, float* ema, float lr, float beta1, float beta2, float eps,
-                    float weight_decay, int step, float ema_rate, void* stream);
+/* torch.optim.AdamW step `step` (>= 1, bias corrections 1 - beta^step) over every parameter with the gradient buffer
+ * (plus grads2, same layout, when not NULL: the second lane's gradients of a batch split over two handles), then
+ * ema = ema_rate * ema + (1 - ema_rate) * params (utils.ema; ema may be NULL) and the bf16 copies */
+int pdm_train_adamw(pdm_trainer* t, float* m, float* v, float* ema, const float* grads2, float lr, float beta1,
+                    float beta2, float eps, float weight_decay, int step, float ema_rate, void* stream);
 /* the backward kernels on their own (parity tests).  pdm_wgrad: C[n][k] (+)= sum_m A[m][n] B[m][k] (bf16 A [M][lda],
  * B [M][ldb], fp32 C [N][ldc]; scratch for split-reduction partials, may be NULL).  pdm_attention_backward: softmax
  * attention over packed qkv [B*L][3*H*Dh] with output o [B*L][H*Dh] and its gradient dout -> dqkv (Dh 64, L <= 288).

@@ -165,7 +165,7 @@ _SIGS = {
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p,
                                       ctypes.c_size_t, ctypes.c_void_p]),
     "pdm_train_adamw": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                       ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                       ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                        ctypes.c_int, ctypes.c_float, ctypes.c_void_p]),
     "pdm_set_wgrad_tile": (ctypes.c_int, [ctypes.c_int]),
     "pdm_wgrad": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,

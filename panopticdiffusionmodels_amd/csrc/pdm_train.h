@@ -18,6 +18,9 @@ struct WgradArgs {
   int M, N, K;
   int mchunk;        // set by wgrad_launch
   int accumulate;
+  // optional: the bias gradient sum_m A[m][n] -> bias_out[n] (+= with bias_acc), from the A tiles the dW GEMM stages
+  // anyway (one MFMA against a ones fragment per A fragment in the k0 == 0 column of tiles); sB: partial stride
+  float* bias_out; int bias_acc; long long sB;
 };
 const char* wgrad_check(const WgradArgs& p);
 extern int g_wgrad_tile;   // 0 = automatic tile, 128 / 256 = forced n-tile (timing A/B)
@@ -89,7 +92,7 @@ hipError_t add_cast_launch(float* dx, const float* add, bf16* dxb, long long n, 
 hipError_t transpose_bf16_launch(const float* w, bf16* wt, int N, int K, hipStream_t stream);
 
 struct AdamWArgs {
-  float* p; const float* g; float* m; float* v; float* ema; bf16* pb;
+  float* p; const float* g; const float* g2; float* m; float* v; float* ema; bf16* pb;   // g2: optional second lane
   float lr, wd, b1, b2, eps, step_size, inv_sqrt_bc2, ema_rate;
 };
 hipError_t adamw_launch(const AdamWArgs& a, long long n, hipStream_t stream);

@@ -175,8 +175,9 @@ int t_gemm(const TC& c, const bf16* A, int lda, const bf16* W, const float* bias
 }
 
 int t_wgrad(const TC& c, const bf16* A, int lda, int N, const bf16* B, int ldb, int K, int M, float* C, int ldc,
-            int a_rpg = 0, int a_gs = 0, int a_off = 0) {
+            float* bias = nullptr, int a_rpg = 0, int a_gs = 0, int a_off = 0) {
   pdm::WgradArgs a{};
+  a.bias_out = bias;   // the bias gradient (column sums of A) fused into the dW GEMM
   a.A = A; a.lda = lda; a.a_rpg = a_rpg; a.a_gs = a_gs; a.a_off = a_off;
   a.B = B; a.ldb = ldb;
   a.C = C; a.ldc = ldc;
@@ -272,17 +273,14 @@ int block_bwd(const TC& c, int b, int rows, float*& DX, bf16*& DXB, float*& DX2,
   const int D = t->D, M = rows * t->L, Hd = t->Hid;
   // x = x1 + fc2(gelu(fc1(norm2(x1))))
   TR_TRY(t_gemm(c, DXB, D, t->wt(pre + ".mlp.fc2.weight"), nullptr, M, Hd, D, pdm::EPI_BF16, w.DG, Hd, nullptr, 0, 0));
-  TR_TRY(t_wgrad(c, DXB, D, D, w.Gl[b], Hd, Hd, M, t->g(pre + ".mlp.fc2.weight"), Hd));
-  TR_TRY(t_colsum(c, DX, 0, D, M, D, t->g(pre + ".mlp.fc2.bias")));
+  TR_TRY(t_wgrad(c, DXB, D, D, w.Gl[b], Hd, Hd, M, t->g(pre + ".mlp.fc2.weight"), Hd, t->g(pre + ".mlp.fc2.bias")));
   TR_HIP(pdm::gelu_bwd_launch(w.DG, w.U[b], (long long)M * Hd, c.s));
   TR_TRY(t_gemm(c, w.DG, Hd, t->wt(pre + ".mlp.fc1.weight"), nullptr, M, D, Hd, pdm::EPI_BF16, w.DH, D, nullptr, 0, 0));
-  TR_TRY(t_wgrad(c, w.DG, Hd, Hd, w.H2[b], D, D, M, t->g(pre + ".mlp.fc1.weight"), D));
-  TR_TRY(t_colsum(c, w.DG, 1, Hd, M, Hd, t->g(pre + ".mlp.fc1.bias")));
+  TR_TRY(t_wgrad(c, w.DG, Hd, Hd, w.H2[b], D, D, M, t->g(pre + ".mlp.fc1.weight"), D, t->g(pre + ".mlp.fc1.bias")));
   TR_TRY(t_ln_bwd(c, w.X1[b], w.DH, 1, pre + ".norm2", DX, DXB, M, 1));
   // x1 = x0 + proj(attn(qkv(norm1(x0))))
   TR_TRY(t_gemm(c, DXB, D, t->wt(pre + ".attn.proj.weight"), nullptr, M, D, D, pdm::EPI_BF16, w.DATT, D, nullptr, 0, 0));
-  TR_TRY(t_wgrad(c, DXB, D, D, w.ATT[b], D, D, M, t->g(pre + ".attn.proj.weight"), D));
-  TR_TRY(t_colsum(c, DX, 0, D, M, D, t->g(pre + ".attn.proj.bias")));
+  TR_TRY(t_wgrad(c, DXB, D, D, w.ATT[b], D, D, M, t->g(pre + ".attn.proj.weight"), D, t->g(pre + ".attn.proj.bias")));
   {
     pdm::AttnBwdArgs a{};
     a.qkv = w.QKV[b]; a.ldq = 3 * D;
@@ -296,15 +294,14 @@ int block_bwd(const TC& c, int b, int rows, float*& DX, bf16*& DXB, float*& DX2,
   }
   TR_TRY(t_gemm(c, w.DQKV, 3 * D, t->wt(pre + ".attn.qkv.weight"), nullptr, M, D, 3 * D, pdm::EPI_BF16, w.DH, D, nullptr,
                 0, 0));
-  TR_TRY(t_wgrad(c, w.DQKV, 3 * D, 3 * D, w.H1[b], D, D, M, t->g(pre + ".attn.qkv.weight"), D));
-  if (t->has(pre + ".attn.qkv.bias")) TR_TRY(t_colsum(c, w.DQKV, 1, 3 * D, M, 3 * D, t->g(pre + ".attn.qkv.bias")));
+  TR_TRY(t_wgrad(c, w.DQKV, 3 * D, 3 * D, w.H1[b], D, D, M, t->g(pre + ".attn.qkv.weight"), D,
+                 t->has(pre + ".attn.qkv.bias") ? t->g(pre + ".attn.qkv.bias") : nullptr));
   TR_TRY(t_ln_bwd(c, w.X0[b], w.DH, 1, pre + ".norm1", DX, DXB, M, 1));
   if (t->skip_block(b)) {   // x0 = skip_linear(cat([x_prev, skip]))
     const int j = t->skip_src(b);
     float* gw = t->g(pre + ".skip_linear.weight");
-    TR_TRY(t_wgrad(c, DXB, D, D, w.XS[b], D, D, M, gw, 2 * D));
+    TR_TRY(t_wgrad(c, DXB, D, D, w.XS[b], D, D, M, gw, 2 * D, t->g(pre + ".skip_linear.bias")));
     TR_TRY(t_wgrad(c, DXB, D, D, w.SK[j], D, D, M, gw + D, 2 * D));
-    TR_TRY(t_colsum(c, DX, 0, D, M, D, t->g(pre + ".skip_linear.bias")));
     const bf16* wt = t->wt(pre + ".skip_linear.weight");   // [2D][D]
     TR_TRY(t_gemm(c, DXB, D, wt + (size_t)D * D, nullptr, M, D, D, pdm::EPI_F32, nullptr, 0, w.DSK[j], D, 0));
     TR_TRY(t_gemm(c, DXB, D, wt, nullptr, M, D, D, pdm::EPI_F32, DXB2, D, DX2, D, 0));
@@ -376,8 +373,7 @@ int train_step(const TC& c, const float* xt, const float* tv, const int64_t* y, 
     a.B = rows; a.D = D; a.C = C; a.p = t->p; a.Himg = S; a.Wimg = S; a.P = t->P; a.P_pad = t->P_pad;
     TR_HIP(pdm::head_bwd_launch(a, c.s));
   }
-  TR_TRY(t_wgrad(c, w.DTOK, t->P_pad, t->P, w.HN, D, D, Mp, t->g("decoder_pred.weight"), D));
-  TR_TRY(t_colsum(c, w.DTOK, 1, t->P_pad, Mp, t->P, t->g("decoder_pred.bias")));
+  TR_TRY(t_wgrad(c, w.DTOK, t->P_pad, t->P, w.HN, D, D, Mp, t->g("decoder_pred.weight"), D, t->g("decoder_pred.bias")));
   float* DX = w.DX;
   float* DX2 = w.DX2;
   bf16* DXB = w.DXB;
@@ -397,9 +393,8 @@ int train_step(const TC& c, const float* xt, const float* tv, const int64_t* y, 
     TR_HIP(pdm::label_scatter_launch(DX, L, 0, D, y, t->g("label_emb.weight"), rows, c.s));
   }
   TR_HIP(pdm::patchify_launch(xt, w.PV, rows, C, S, S, t->p, t->Kp_pad, c.s));
-  TR_TRY(t_wgrad(c, DXB, D, D, w.PV, t->Kp_pad, t->Kp, Mp, t->g("patch_embed.proj.weight"), t->Kp, t->n_patch, L,
-                 t->extras));
-  TR_TRY(t_colsum(c, DX, 0, D, Mp, D, t->g("patch_embed.proj.bias"), t->n_patch, L, t->extras));
+  TR_TRY(t_wgrad(c, DXB, D, D, w.PV, t->Kp_pad, t->Kp, Mp, t->g("patch_embed.proj.weight"), t->Kp,
+                 t->g("patch_embed.proj.bias"), t->n_patch, L, t->extras));
   return PDM_OK;
 }
 
@@ -537,12 +532,12 @@ int pdm_train_step(pdm_trainer* t, const float* xt, const float* tvals, const in
   return train_step(c, xt, tvals, y, target, loss, rows, gscale);
 }
 
-int pdm_train_adamw(pdm_trainer* t, float* m, float* v, float* ema, float lr, float beta1, float beta2, float eps,
-                    float weight_decay, int step, float ema_rate, void* stream) {
+int pdm_train_adamw(pdm_trainer* t, float* m, float* v, float* ema, const float* grads2, float lr, float beta1,
+                    float beta2, float eps, float weight_decay, int step, float ema_rate, void* stream) {
   if (!t || !t->Pm) return pdm::set_error(PDM_ERR_STATE, "pdm_train_adamw: buffers not set");
   if (!m || !v || step < 1) return pdm::set_error(PDM_ERR_ARG, "pdm_train_adamw: moments missing or step < 1");
   pdm::AdamWArgs a{};
-  a.p = t->Pm; a.g = t->G; a.m = m; a.v = v; a.ema = ema; a.pb = nullptr;
+  a.p = t->Pm; a.g = t->G; a.g2 = grads2; a.m = m; a.v = v; a.ema = ema; a.pb = nullptr;
   a.lr = lr; a.wd = weight_decay; a.b1 = beta1; a.b2 = beta2; a.eps = eps;
   const double bc1 = 1.0 - std::pow((double)beta1, step), bc2 = 1.0 - std::pow((double)beta2, step);
   a.step_size = (float)(lr / bc1);

@@ -120,6 +120,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p, int tiles_k)
   for (int i = 0; i < KI; ++i)
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // bias gradient: the k0 == 0 column of tiles also sums its A columns (wk == 0 waves: one copy per n)
+  const bool do_bias = p.bias_out != nullptr && tk == 0 && wk == 0;
+  f32x4 bacc[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) bacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones8[j] = (bf16)1.0f;
 
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
   const int r1 = g * 8 + qq, r2 = r1 + 4;
@@ -148,12 +156,20 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p, int tiles_k)
     for (int ki = 0; ki < KI; ++ki)
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) acc[ki][ni] = mfma16x16x32(bfr[ki], af[ni], acc[ki][ni]);
+    if (do_bias) {
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) bacc[ni] = mfma16x16x32(ones8, af[ni], bacc[ni]);
+    }
   }
   // lane: column n = .. + (lane & 15), 4 consecutive k = .. + (lane >> 4) * 4
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) {
     const int n = n0 + wn * 64 + ni * 16 + i16;
     if (n >= p.N) continue;
+    if (do_bias && g == 0) {   // every output row of the ones product holds the column sum
+      float* bd = p.bias_out + (long long)blockIdx.y * p.sB + n;
+      *bd = p.bias_acc ? *bd + bacc[ni][0] : bacc[ni][0];
+    }
 #pragma unroll
     for (int ki = 0; ki < KI; ++ki) {
       const int k = k0 + wk * 64 + ki * 16 + g * 4;
@@ -275,15 +291,22 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs p, const DT* dh) 
       }
     }
   }
-  float* pg = p.part + (size_t)gw * p.D;                    // dgamma partials [nw][D]
-  float* pb = p.part + ((size_t)nw + gw) * p.D;             // dbeta partials  [nw][D]
+  // the block's four waves' partials summed through LDS: one dgamma / dbeta partial row per block
+  // (partials [2][gridDim.x][D]; fewer rows for the column-sum passes that follow)
+  __shared__ f32x4 red[4][2][64];
+  float* pg = p.part + (size_t)blockIdx.x * p.D;                          // dgamma partials [nblk][D]
+  float* pb = p.part + ((size_t)gridDim.x + blockIdx.x) * p.D;            // dbeta partials  [nblk][D]
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int idx = lane + i * 64;
-    if (idx < nv) {
-      reinterpret_cast<f32x4*>(pg)[idx] = dg[i];
-      reinterpret_cast<f32x4*>(pb)[idx] = db[i];
+    red[wave][0][lane] = dg[i];
+    red[wave][1][lane] = db[i];
+    __syncthreads();
+    if (wave < 2) {
+      const f32x4 v = red[0][wave][lane] + red[1][wave][lane] + red[2][wave][lane] + red[3][wave][lane];
+      const int idx = lane + i * 64;
+      if (idx < nv) reinterpret_cast<f32x4*>(wave == 0 ? pg : pb)[idx] = v;
     }
+    __syncthreads();
   }
 }
 
@@ -687,7 +710,7 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const float* w, bf1
 // p <- p - (lr / bc1) m / (sqrt(v) / sqrt(bc2) + eps);  ema <- rate ema + (1 - rate) p;  pb <- bf16(p)
 __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a, long long n) {
   for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
-    const float g = a.g[e];
+    const float g = a.g2 ? a.g[e] + a.g2[e] : a.g[e];
     float pv = a.p[e] * (1.0f - a.lr * a.wd);
     const float m = a.b1 * a.m[e] + (1.0f - a.b1) * g;
     const float v = a.b2 * a.v[e] + (1.0f - a.b2) * g * g;
@@ -706,6 +729,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a, long long n) {
 const char* wgrad_check(const WgradArgs& p) {
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return "wgrad: M, N, K must be positive";
   if (p.K % 4 || p.ldc % 4) return "wgrad: K and ldc must be multiples of 4";
+  if (p.bias_out && p.N % 4) return "wgrad: the fused bias gradient needs N % 4 == 0";
   if (p.lda % 8 || p.ldb % 8) return "wgrad: lda / ldb must be multiples of 8 (16-byte rows)";
   if (((uintptr_t)p.A | (uintptr_t)p.B) & 15 || ((uintptr_t)p.C & 15)) return "wgrad: operands must be 16-byte aligned";
   const long long arows = p.a_rpg > 0 ? (long long)((p.M - 1) / p.a_rpg) * p.a_gs + p.a_off + p.a_rpg : p.M;
@@ -728,8 +752,9 @@ hipError_t wgrad_launch(const WgradArgs& args, float* part, size_t part_bytes, h
   int split = (1024 + tiles - 1) / tiles;
   split = std::min(split, std::max(1, p.M / 512));
   const long long nk = (long long)p.N * p.K;
+  const long long nb = p.bias_out ? p.N : 0;   // bias partials follow the dW partials
   if (!part) split = 1;
-  else split = (int)std::min<long long>(split, (long long)(part_bytes / (nk * 4)));
+  else split = (int)std::min<long long>(split, (long long)(part_bytes / ((nk + nb) * 4)));
   if (split < 1) split = 1;
   int mchunk = ((p.M + split - 1) / split + 31) & ~31;
   split = (p.M + mchunk - 1) / mchunk;
@@ -739,8 +764,14 @@ hipError_t wgrad_launch(const WgradArgs& args, float* part, size_t part_bytes, h
     p.ldc = p.K;
     p.sC = nk;
     p.accumulate = 0;
+    if (p.bias_out) {
+      p.bias_out = part + (size_t)split * nk;
+      p.sB = p.N;
+      p.bias_acc = 0;
+    }
   } else {
     p.sC = 0;
+    p.sB = 0;
   }
   if (TN == 256)
     hipLaunchKernelGGL(wgrad_kernel<256>, dim3(tiles, split), dim3(256), 3 * (32 * 256 * 2 + 32 * 128 * 2), stream, p,
@@ -751,6 +782,9 @@ hipError_t wgrad_launch(const WgradArgs& args, float* part, size_t part_bytes, h
   if (e != hipSuccess || split == 1) return e;
   hipLaunchKernelGGL(reduce_parts_kernel, dim3(grid_for(nk / 4)), dim3(256), 0, stream, part, split, p.N, p.K, args.C,
                      args.ldc, args.accumulate);
+  if ((e = hipGetLastError()) != hipSuccess || !args.bias_out) return e;
+  hipLaunchKernelGGL(reduce_parts_kernel, dim3(grid_for(p.N / 4)), dim3(256), 0, stream, p.bias_out, split, 1, p.N,
+                     args.bias_out, p.N, args.bias_acc);
   return hipGetLastError();
 }
 
@@ -810,8 +844,8 @@ hipError_t ln_bwd_launch(const LnBwdArgs& args, const void* dh, int dh_bf16, flo
 #undef PDM_LNB
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // partials [2][nw][D] in the first part of the scratch; the column sums use the rest
-  const int nw = nblk * 4;
+  // partials [2][nblk][D] in the first part of the scratch; the column sums use the rest
+  const int nw = nblk;
   float* rest = p.part + (size_t)2 * nw * p.D;
   const size_t rest_bytes = p.part_bytes - (size_t)2 * nw * p.D * 4;
   if ((e = colsum_launch(p.part, 0, p.D, nw, p.D, 0, 0, 0, dgamma, p.accumulate_params, rest, rest_bytes, stream)) !=

@@ -71,7 +71,11 @@ class HipTrainState:
     `state_dict()` / `ema_state_dict()` hand back reference-keyed tensors (views copied out), so checkpoints
     interoperate with utils.TrainState's nnet / nnet_ema files."""
 
-    def __init__(self, nnet_kwargs, device="cuda", optimizer=None, lr_scheduler=None, ema_rate=0.9999):
+    def __init__(self, nnet_kwargs, device="cuda", optimizer=None, lr_scheduler=None, ema_rate=0.9999, lanes=1):
+        """lanes=2 splits each batch into two halves run concurrently on their own streams (a second pdm_train
+        handle sharing the parameters and bf16 copies, with its own workspace and gradient buffer; AdamW sums the
+        two), so one half's GEMM tiles fill the CUs the other half's partly filled last wave leaves idle -- the
+        sampler lanes (sampler.py) applied to the training step."""
         _lib.require_gpu()
         kw = dict(nnet_kwargs)
         if kw.pop("name", "uvit") != "uvit":
@@ -113,11 +117,25 @@ class HipTrainState:
         self.step = 0
         self.shapes = {}
         self.ws = None
+        self.lanes = max(1, min(2, int(lanes)))
+        self.h2 = self.G2 = self.ws2 = None
+        self._streams = []
+        if self.lanes == 2:
+            h2 = ctypes.c_void_p()
+            _lib.check(self.lib.pdm_train_create(ctypes.byref(cfg_struct(kw, False)), ctypes.byref(h2)),
+                       "pdm_train_create")
+            self.h2 = h2
+            self.G2 = torch.zeros(self.n, dtype=torch.float32, device=dev)
+            _lib.check(self.lib.pdm_train_set_buffers(h2, _lib.ptr(self.P), _lib.ptr(self.G2), _lib.ptr(self.WB),
+                                                      _lib.ptr(self.WT)), "pdm_train_set_buffers")
+            self._streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
 
     def __del__(self):
         try:
             if getattr(self, "h", None):
                 self.lib.pdm_train_destroy(self.h)
+            if getattr(self, "h2", None):
+                self.lib.pdm_train_destroy(self.h2)
         except Exception:
             pass
 
@@ -150,16 +168,32 @@ class HipTrainState:
         return {k: self._view(self.E, k).clone() for k in self.index}
 
     def grads(self):
-        return {k: self._view(self.G, k).clone() for k in self.index}
+        g = self.G + self.G2 if self.G2 is not None else self.G
+        return {k: self._view(g, k).clone() for k in self.index}
 
     # ---- one step --------------------------------------------------------------------------------------------
-    def _workspace(self, rows):
+    def _workspace(self, rows, lane=0):
         need = ctypes.c_size_t()
         _lib.check(self.lib.pdm_train_workspace_size(self.h, rows, ctypes.byref(need)), "pdm_train_workspace_size")
-        if self.ws is None or self.ws.numel() < need.value:
-            self.ws = None
-            self.ws = torch.empty(need.value, dtype=torch.uint8, device=self.device)
-        return self.ws
+        ws = self.ws if lane == 0 else self.ws2
+        if ws is None or ws.numel() < need.value:
+            ws = None
+            if lane == 0:
+                self.ws = None
+            else:
+                self.ws2 = None
+            ws = torch.empty(need.value, dtype=torch.uint8, device=self.device)
+            if lane == 0:
+                self.ws = ws
+            else:
+                self.ws2 = ws
+        return ws
+
+    def _step_call(self, h, xt, t_in, y, target, loss, gscale, ws, stream):
+        B = xt.shape[0]
+        _lib.check(self.lib.pdm_train_step(h, _lib.ptr(xt), _lib.ptr(t_in), _lib.ptr(y), _lib.ptr(target),
+                                           _lib.ptr(loss), B, float(gscale), _lib.ptr(ws), ws.numel(),
+                                           ctypes.c_void_p(stream.cuda_stream)), "pdm_train_step")
 
     def forward_backward(self, xt, t_in, y, target, gscale=None):
         """loss[b] = mos(target - nnet(xt, t_in, y)) and d(gscale * sum(loss)) / d(params) into the gradient buffer
@@ -170,23 +204,48 @@ class HipTrainState:
         t_in = t_in.to(self.device, torch.float32).contiguous().reshape(B)
         if y is not None:
             y = y.to(self.device, torch.int64).contiguous()
+        gs = float(1.0 / B if gscale is None else gscale)
         loss = torch.empty(B, dtype=torch.float32, device=self.device)
-        ws = self._workspace(B)
-        _lib.check(self.lib.pdm_train_step(self.h, _lib.ptr(xt), _lib.ptr(t_in), _lib.ptr(y), _lib.ptr(target),
-                                           _lib.ptr(loss), B, float(1.0 / B if gscale is None else gscale),
-                                           _lib.ptr(ws), ws.numel(), _lib.stream_ptr(self.device)), "pdm_train_step")
+        cur = torch.cuda.current_stream(self.device)
+        if self.lanes == 1 or B < 2:
+            if self.G2 is not None:
+                self.G2.zero_()
+            self._step_call(self.h, xt, t_in, y, target, loss, gs, self._workspace(B), cur)
+            return loss
+        h0 = B // 2
+        parts = [(0, h0), (h0, B)]
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        for lane, (a, b) in enumerate(parts):
+            s = self._streams[lane]
+            s.wait_event(ready)
+            ws = self._workspace(b - a, lane)
+            with torch.cuda.stream(s):
+                self._step_call(self.h if lane == 0 else self.h2, xt[a:b], t_in[a:b],
+                                y[a:b] if y is not None else None, target[a:b], loss[a:b], gs, ws, s)
+            done = torch.cuda.Event()
+            done.record(s)
+            cur.wait_event(done)
+            for t in (xt, t_in, target, loss, ws) + ((y,) if y is not None else ()):
+                t.record_stream(s)
         return loss
 
     def all_reduce_grads(self):
-        """DDP: average the gradient buffer over the process group (RCCL on the GPU)."""
-        average_gradients(self.G)
+        """DDP: average the gradient buffer over the process group (RCCL on the GPU); with two lanes the second
+        lane's gradients are folded in first (at world size 1 AdamW sums the two buffers itself)."""
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            if self.G2 is not None:
+                self.G.add_(self.G2)
+                self.G2.zero_()
+            average_gradients(self.G)
 
     def optimizer_step(self):
         """AdamW at the current scheduled LR, then the EMA update; advances the step counter."""
         o = self.optimizer
         lr = customized_lr(o["lr"], self.step, self.lr_scheduler.get("warmup_steps", -1))
         b1, b2 = o["betas"]
-        _lib.check(self.lib.pdm_train_adamw(self.h, _lib.ptr(self.M), _lib.ptr(self.V), _lib.ptr(self.E), float(lr),
+        _lib.check(self.lib.pdm_train_adamw(self.h, _lib.ptr(self.M), _lib.ptr(self.V), _lib.ptr(self.E),
+                                            _lib.ptr(self.G2), float(lr),
                                             float(b1), float(b2), float(o.get("eps", 1e-8)), float(o["weight_decay"]),
                                             self.step + 1, float(self.ema_rate), _lib.stream_ptr(self.device)),
                    "pdm_train_adamw")

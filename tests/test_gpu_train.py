@@ -202,3 +202,34 @@ def test_train_step_batch_invariance():
     assert torch.allclose(l2[:3], l1, rtol=1e-5, atol=1e-7) and torch.allclose(l2[3:], l1, rtol=1e-5, atol=1e-7)
     for k in g1:
         assert rel(g2[k], g1[k]) < 1e-3 or float(g1[k].norm()) == 0, k
+
+
+def test_train_lanes_equal_single():
+    """Two concurrent half-batch lanes (HipTrainState lanes=2) give the single-lane losses and gradients (only the
+    fp32 summation order of the token reduction differs), and the same parameters after an AdamW step."""
+    from panopticdiffusionmodels_amd import configs, weights
+    from panopticdiffusionmodels_amd.train import HipTrainState
+    full = configs.get_config("tiny_uvit_train")
+    sd = weights.nnet_state_dict(full["nnet"], seed=11, init="random")
+    sts = []
+    for lanes in (1, 2):
+        st = HipTrainState(full["nnet"], DEV, optimizer=full["optimizer"], lr_scheduler=dict(warmup_steps=-1),
+                           ema_rate=0.9, lanes=lanes)
+        st.load_state_dict(sd)
+        sts.append(st)
+    g = torch.Generator().manual_seed(4)
+    xt = torch.randn(5, 4, 16, 16, generator=g)
+    t = torch.rand(5, generator=g) * 999
+    y = torch.tensor([1, 4, 10, 0, 7])
+    eps = torch.randn(5, 4, 16, 16, generator=g)
+    losses = [st.forward_backward(xt, t, y, eps).cpu() for st in sts]
+    assert torch.allclose(losses[0], losses[1], rtol=1e-5, atol=1e-7)
+    g1, g2 = sts[0].grads(), sts[1].grads()
+    for k in g1:
+        assert rel(g2[k], g1[k]) < 1e-4 or float(g1[k].norm()) == 0, k
+    for st in sts:
+        st.optimizer_step()
+    p1, p2 = sts[0].state_dict(), sts[1].state_dict()
+    num = sum(float((p2[k].double() - p1[k].double()).norm() ** 2) for k in p1)
+    den = sum(float((p1[k].double() - sd[k].double().to(p1[k].device)).norm() ** 2) for k in p1)
+    assert (num / den) ** 0.5 < 0.05
