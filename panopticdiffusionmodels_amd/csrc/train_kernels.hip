@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(bf16* dg, const bf16* u, 
 
 // ------------------------------------------------------------------------------------------------
 // Attention backward (libs/uvit.py:66-92 with S = Q K^T Dh^-1/2, P = softmax(S), O = P V), Dh = 64, L <= 288.
-// One workgroup (8 waves) per (sequence b, head h); Q, K, V and dO of the head live in LDS as [Lp][64] bf16 images
+// One workgroup (16 waves) per (sequence b, head h); Q, K, V and dO of the head live in LDS as [Lp][64] bf16 images
 // (128-B rows, 16-B chunk c of row r stored at c ^ (r & 7)), Lp = L rounded up to 32, rows >= L zero.
 //   pass 0: lse2[q] = log2 sum_k exp2(S c) (c = Dh^-1/2 log2 e; +inf for padded queries) and
 //           delta[q] = sum_d dO[q][d] O[q][d]
@@ -350,6 +350,7 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(bf16* dg, const bf16* u, 
 //   pass B: per 16-query tile (wave-owned): over 32-key slices S^T, P^T, dP^T, dS^T, dQ^T += K^T dS^T
 // dK, dQ are scaled by Dh^-1/2.  Output: dqkv [b*L + i][3D] in the (3, H, Dh) column layout of the forward's qkv.
 constexpr int AB_MAXL = 288;
+constexpr int AB_THREADS = 1024;   // one workgroup per (image, head): 16 waves over its 16-key / 16-query tiles
 
 __device__ __forceinline__ int ab_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
@@ -366,7 +367,8 @@ __device__ __forceinline__ bf16x8 ab_trT(const char* img, int r0, int d0, int la
   return tr_frag(img + ab_off(ra, c) + (p & 1) * 8, img + ab_off(rb, c) + (p & 1) * 8);
 }
 
-__global__ __launch_bounds__(512, 1) void attn_bwd_kernel(AttnBwdArgs p) {
+__global__ __launch_bounds__(AB_THREADS, 1) void attn_bwd_kernel(AttnBwdArgs p) {
+  constexpr int NWV = AB_THREADS / 64;   // waves: 16 = four per SIMD (120 VGPRs each)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = p.L, Lp = (L + 31) & ~31;
   const int bh = blockIdx.x, b = bh / p.H, h = bh - b * p.H;
@@ -381,7 +383,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(AttnBwdArgs p) {
   const size_t row0 = (size_t)b * L;
 
   // stage Q, K, V, dO (16-B chunks, rows >= L zero)
-  for (int e = tid; e < Lp * 8 * 4; e += 512) {
+  for (int e = tid; e < Lp * 8 * 4; e += AB_THREADS) {
     const int img = e / (Lp * 8), r = (e / 8) % Lp, c = e & 7;
     bf16x8 v = bf16x8{};
     if (r < L) {
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(AttnBwdArgs p) {
   const int g = lane >> 4, col = lane & 15;
 
   // ---- pass 0: lse2 per query (16-query tiles), delta per query
-  for (int qt = wave; qt * 16 < Lp; qt += 8) {
+  for (int qt = wave; qt * 16 < Lp; qt += NWV) {
     const int q0 = qt * 16;
     float m = -INFINITY, l = 0.f;
     for (int k0 = 0; k0 < Lp; k0 += 16) {
@@ -424,7 +426,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(AttnBwdArgs p) {
     }
     if (g == 0) lse[q0 + col] = (q0 + col < L) ? m + log2f(l) : INFINITY;
   }
-  for (int q = tid; q < Lp; q += 512) {
+  for (int q = tid; q < Lp; q += AB_THREADS) {
     float d = 0.f;
     if (q < L) {
       const bf16* orow = p.o + (row0 + q) * p.ldo + h * 64;
@@ -441,7 +443,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(AttnBwdArgs p) {
   __syncthreads();
 
   // ---- pass A: dK, dV per 16-key tile
-  for (int kt = wave; kt * 16 < L; kt += 8) {
+  for (int kt = wave; kt * 16 < L; kt += NWV) {
     const int k0 = kt * 16;
     f32x4 dv[4], dk[4];
 #pragma unroll
@@ -490,7 +492,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(AttnBwdArgs p) {
   }
 
   // ---- pass B: dQ per 16-query tile
-  for (int qt = wave; qt * 16 < L; qt += 8) {
+  for (int qt = wave; qt * 16 < L; qt += NWV) {
     const int q0 = qt * 16;
     const int q = q0 + col;
     const float lq = lse[q], dq_ = dlt[q];
@@ -884,7 +886,7 @@ hipError_t attn_bwd_launch(const AttnBwdArgs& p, hipStream_t stream) {
                               4 * AB_MAXL * 128 + 2 * AB_MAXL * 4);
     attr = true;
   }
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(p.B * p.H), dim3(512), smem, stream, p);
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(p.B * p.H), dim3(AB_THREADS), smem, stream, p);
   return hipGetLastError();
 }
 
