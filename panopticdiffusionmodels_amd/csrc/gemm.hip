@@ -243,10 +243,27 @@ __device__ __forceinline__ float2 ln_from_partials(const float2 (&lst)[8], int l
   return make_float2(mean, 1.0f / sqrtf(m2 / (float)D + eps));
 }
 
+// Sum over each 32-lane half of the wave, bitwise the same in every lane (each step adds two equal-valued partners,
+// so the commuted sums agree): two quad_perm butterflies, row_half_mirror (quad 0 <-> 1, 2 <-> 3) and row_mirror
+// (8-lane halves) as VALU adds with a DPP source (no LDS traffic) for the 16-lane rows, then one swizzle across the
+// two rows of each half (v_permlane16_swap measured wrong for this: tools/probes/dpp_probe.hip).
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float x) {
+  return x + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float sum32(float x) {
+  x = dpp_add<0xb1>(x);    // quad_perm [1,0,3,2]
+  x = dpp_add<0x4e>(x);    // quad_perm [2,3,0,1]
+  x = dpp_add<0x141>(x);   // row_half_mirror
+  x = dpp_add<0x140>(x);   // row_mirror
+  return x + __shfl_xor(x, 16, 64);
+}
+
 // Epilogue of a 256x256 tile (needs 128 KiB of LDS; the staging ring is free by then).
 //  EPI_RES: the fp32 path below with a bf16 residual stream (res_in read, bf16 out_bf16 written, 16-byte rows).
 //  bf16 / GELU: the bf16 tile is written to LDS with a row-XOR chunk swizzle, then stored row-contiguously
-//    with 16-byte stores (full lines, half the store instructions of the per-lane 8-byte scatter).
+//    with 16-byte stores (full lines, half the store instructions of the per-lane 8-byte scatter).  Non-temporal
+//    (streaming) stores measured neutral (profiles/r03nt/: qkv 149.1 vs 149.0 us, L/2 bench 57.9 vs 58.0 img/s).
 //  fp32 residual: two 128-row passes through LDS; every thread then owns 8 consecutive columns of a row:
 //    2 x 16-byte residual loads, 2 x 16-byte stores and one 16-byte bf16 copy store per row chunk.
 template <int EPI, int MAP>
@@ -376,8 +393,7 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
       sv += n + j < p.N ? a[j] : 0.f;
       sv += n + 4 + j < p.N ? b[j] : 0.f;
     }
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) sv += __shfl_xor(sv, o, 64);
+    sv = sum32(sv);
     const float mu = sv / (float)ncols;
     float q = 0.f;
 #pragma unroll
@@ -386,8 +402,7 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
       q += n + j < p.N ? d0 * d0 : 0.f;
       q += n + 4 + j < p.N ? d1 * d1 : 0.f;
     }
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    q = sum32(q);
     if ((tid & 31) == 0 && m < p.M)
       *reinterpret_cast<float2*>(p.stats_out + ((size_t)m * p.stats_ld + (n0 >> 8)) * 2) = make_float2(sv, q);
     return mu;
