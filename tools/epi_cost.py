@@ -11,6 +11,8 @@ from panopticdiffusionmodels_amd import _lib  # noqa: E402
 lib = _lib.load()
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 190
 D = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+ALGO = int(sys.argv[3]) if len(sys.argv) > 3 else 0   # GEMM tile policy (pdm_set_gemm_algo; 0 = automatic)
+lib.pdm_set_gemm_algo(ALGO)
 L = 258
 M = rows * L
 dev = "cuda"
