@@ -1933,6 +1933,11 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
     return launch_mx(p, epi, stream);
   }
   if (p.out_fp8) algo = 7;   // MXFP8 output lives in the 256-tile epilogue
+  // no-store timing mode (pdm_set_gemm_tuning bit 1, gemm_check): only the 256-tile epilogue skips a missing output
+  if ((epi == EPI_BF16 || epi == EPI_GELU) && !p.out_bf16 && !p.out_fp8) {
+    if (!fits_rsrc(p) || p.conv || p.batch > 1) return hipErrorInvalidValue;
+    algo = 7;
+  }
   // operands past the descriptor kernels' 2 GiB byte-offset range (e.g. a 32-image chunk of 512^2 x 256-channel
   // conv inputs): split the rows into parts that fit -- whole images for a conv -- instead of dropping to the
   // 128-tile kernel
