@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* x, const float* 
   const T* xb = x + (size_t)b * P * C + c;
   bf16* yb = y + (size_t)b * P * C + c;
   const int step = gridDim.x * planes;
-#pragma unroll 2
+#pragma unroll 4
   for (int pi = blockIdx.x * planes + plane; pi < P; pi += step) {
     float v[8];
     if constexpr (sizeof(T) == 4) {
@@ -471,7 +471,9 @@ int groupnorm(const DCtx& c, const T* x, int B, int P, int C, const std::string&
                      (double)P * (C / 32), 1e-6f, c.w->stats, B);
   if (C % 8 || C > 2048) return dfail(PDM_ERR_ARG, "decoder: GroupNorm needs C % 8 == 0 and C <= 2048");
   const int planes = 256 / (C / 8);
-  const int gx = std::max(1, std::min((P + planes - 1) / planes, 2048 / B + 1));   // >= ~2048 blocks in flight
+  // >= ~8192 blocks (up to 32 waves per CU): the pixel loop keeps 4 pixels' loads in flight per thread, and at
+  // ~2048 blocks the fp32 apply streamed at ~2.5 TB/s (512^2 decode, profiles/r03r_dec512_kernel_stats.csv)
+  const int gx = std::max(1, std::min((P + planes - 1) / planes, 8192 / B + 1));
   hipLaunchKernelGGL(pdm::gn_apply_kernel<T>, dim3(gx, B), dim3(256), 0, c.s, x, c.w->stats,
                      c.d->f(norm + ".weight"), c.d->f(norm + ".bias"), y, P, C, swish ? 1 : 0);
   D_HIP(hipGetLastError());
