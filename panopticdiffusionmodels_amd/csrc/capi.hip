@@ -655,16 +655,19 @@ int t2i_two_stream16(const Ctx& c, const Workspace& w, int rows, int use_ground_
   const pdm_uvit* h = c.h;
   const int D = h->D, Lx = h->Lx, Lm = h->Lm, n = h->nhalf, T = (D + 255) / 256;
   const size_t MDx = (size_t)rows * Lx * D, MDm = (size_t)rows * Lm * D;
-  // bf16 row copies of D columns (as fp32 words: D / 2 per row)
-  auto copy_rows = [&](bf16* dst, const bf16* src, int rpg, int dgs, int sgs) -> int {
-    PDM_HIP(pdm::rowcopy_launch((float*)dst, D / 2, (const float*)src, D / 2, rows * rpg, D / 2, rpg, dgs, sgs, c.s));
+  // bf16 row copies of D columns (as fp32 words: D / 2 per row), optionally with the rows' LayerNorm partials
+  auto copy_rows = [&](bf16* dst, const bf16* src, int rpg, int dgs, int sgs, float* st_dst = nullptr,
+                       const float* st_src = nullptr) -> int {
+    PDM_HIP(pdm::rowcopy_launch((float*)dst, D / 2, (const float*)src, D / 2, rows * rpg, D / 2, rpg, dgs, sgs, c.s,
+                                st_dst, 2 * T, st_src, 2 * T, 2 * T));
     return PDM_OK;
   };
-  // mb = cat(x_img, m_src[:, Lx:]) + its partials (m_src == MB: the mask rows are already in place)
+  // mb = cat(x_img, m_src[:, Lx:]) + its partials (m_src == MB: the mask rows are already in place).  The mask
+  // rows' LayerNorm partials are already in STM (written there by the mask block that produced m_src, in its fc2
+  // epilogue, or by the token assembly); the image rows' are x's own (ST, from the injection GEMM / the assembly).
   auto refresh = [&](const bf16* x_img, const bf16* m_src) -> int {
-    PDM_TRY(copy_rows(w.MB, x_img, Lx, Lm, Lx));
+    PDM_TRY(copy_rows(w.MB, x_img, Lx, Lm, Lx, w.STM, w.ST));
     if (m_src != w.MB) PDM_TRY(copy_rows(w.MB + (size_t)Lx * D, m_src + (size_t)Lx * D, Lm - Lx, Lm, Lm));
-    PDM_HIP(pdm::rowstats_bf16_launch(w.MB, D, rows * Lm, D, w.STM, T, c.s));
     return PDM_OK;
   };
   auto inject = [&](int layer, const bf16* mout, const bf16* x_res, bf16* x_out) -> int {
@@ -687,25 +690,26 @@ int t2i_two_stream16(const Ctx& c, const Workspace& w, int rows, int use_ground_
   int layer = 0;
   // Per layer the mask block runs first (its input only needs the image block's INPUT x), then the image block,
   // whose output stays in XT (its proj / fc2 update XT in place), then the injection writes the layer's x.  The
-  // blocks' own output partials are not needed: the injection and the next refresh produce them.
+  // mask block's fc2 writes its output's partials into STM (the next refresh keeps the mask rows' ones); the
+  // image block's are not needed (the injection produces x's).
   for (int i = 0; i < n; ++i, ++layer) {
     PDM_TRY(refresh(x, m));
     PDM_TRY(run_block16(c, "in_blocks_mask." + std::to_string(i), rows, Lm, w.MB, w.STM, nullptr, w.SKM + i * MDm,
-                        nullptr, w));
+                        w.STM, w));
     PDM_TRY(run_block16(c, "in_blocks." + std::to_string(i), rows, Lx, x, w.ST, nullptr, w.XT, nullptr, w));
     PDM_TRY(inject(layer, w.SKM + i * MDm, w.XT, w.SK + i * MDx));
     x = w.SK + i * MDx;
     m = w.SKM + i * MDm;
   }
   PDM_TRY(refresh(x, m));
-  PDM_TRY(run_block16(c, "mid_block_mask", rows, Lm, w.MB, w.STM, nullptr, w.MXB, nullptr, w));
+  PDM_TRY(run_block16(c, "mid_block_mask", rows, Lm, w.MB, w.STM, nullptr, w.MXB, w.STM, w));
   PDM_TRY(run_block16(c, "mid_block", rows, Lx, x, w.ST, nullptr, w.XT, nullptr, w));
   PDM_TRY(inject(layer, w.MXB, w.XT, w.XB));
   ++layer;
   for (int i = 0; i < n; ++i, ++layer) {
     PDM_TRY(refresh(w.XB, w.MXB));
     const bf16* skm = h->cfg.skip ? w.SKM + (n - 1 - i) * MDm : nullptr;
-    PDM_TRY(run_block16(c, "out_blocks_mask." + std::to_string(i), rows, Lm, w.MB, w.STM, skm, w.MXB, nullptr, w));
+    PDM_TRY(run_block16(c, "out_blocks_mask." + std::to_string(i), rows, Lm, w.MB, w.STM, skm, w.MXB, w.STM, w));
     const bf16* sk = h->cfg.skip ? w.SK + (n - 1 - i) * MDx : nullptr;
     PDM_TRY(run_block16(c, "out_blocks." + std::to_string(i), rows, Lx, w.XB, w.ST, sk, w.XT, nullptr, w));
     PDM_TRY(inject(layer, w.MXB, w.XT, w.XB));

@@ -351,14 +351,26 @@ __global__ __launch_bounds__(256) void lincomb_kernel(float* out, int n_terms, L
   }
 }
 
+// one wave per row (4 rows per block): the row's D floats as 16-byte chunks when rows and pointers allow, else
+// scalar; optionally a second, narrow row with the same row mapping (the row's LayerNorm partials)
 __global__ __launch_bounds__(256) void rowcopy_kernel(float* dst, int ldd, const float* src, int lds, int rows, int D,
-                                                     int rpg, int dgs, int sgs) {
-  const int r = blockIdx.x;
+                                                     int rpg, int dgs, int sgs, float* dst2, int ldd2,
+                                                     const float* src2, int lds2, int D2) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= rows) return;
   const int grp = r / rpg, k = r % rpg;
-  const f32x4* s = reinterpret_cast<const f32x4*>(src + ((size_t)grp * sgs + k) * lds);
-  f32x4* d = reinterpret_cast<f32x4*>(dst + ((size_t)grp * dgs + k) * ldd);
-  for (int j = threadIdx.x; j < (D >> 2); j += 256) d[j] = s[j];
+  const size_t ds = (size_t)grp * dgs + k, ss = (size_t)grp * sgs + k;
+  const float* sr = src + ss * lds;
+  float* dr = dst + ds * ldd;
+  if (((D | ldd | lds) & 3) == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(sr);
+    f32x4* d4 = reinterpret_cast<f32x4*>(dr);
+    for (int j = lane; j < (D >> 2); j += 64) d4[j] = s4[j];
+  } else {
+    for (int j = lane; j < D; j += 64) dr[j] = sr[j];
+  }
+  if (dst2)
+    for (int j = lane; j < D2; j += 64) dst2[ds * ldd2 + j] = src2[ss * lds2 + j];
 }
 
 // fp32 -> bf16 (round to nearest even).  Eight elements per thread when x and y are 16-B aligned: two
@@ -544,9 +556,11 @@ hipError_t mxq_launch(const void* x, int dtype, int ldx, int rows, int K, unsign
 }
 
 hipError_t rowcopy_launch(float* dst, int ldd, const float* src, int lds, int rows, int D, int rows_per_group,
-                          int dst_group_stride, int src_group_stride, hipStream_t stream) {
-  hipLaunchKernelGGL(rowcopy_kernel, dim3(rows), dim3(256), 0, stream, dst, ldd, src, lds, rows, D, rows_per_group,
-                     dst_group_stride, src_group_stride);
+                          int dst_group_stride, int src_group_stride, hipStream_t stream, float* dst2, int ldd2,
+                          const float* src2, int lds2, int D2) {
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rowcopy_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, dst, ldd, src, lds, rows, D,
+                     rows_per_group, dst_group_stride, src_group_stride, dst2, ldd2, src2, lds2, D2);
   return hipGetLastError();
 }
 

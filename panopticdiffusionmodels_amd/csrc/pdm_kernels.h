@@ -193,8 +193,11 @@ hipError_t mxq_launch(const void* x, int dtype, int ldx, int rows, int K, unsign
 // out = sum_i c_i * T_i over n elements (fp32); used by the generic solver path.
 hipError_t lincomb_launch(float* out, int n_terms, const float* const* T, const float* c, long long n, hipStream_t stream);
 
-// Strided row copy fp32: dst[r*ldd + j] = src[r*lds + j], j < D, r < rows (t2i mask stream concat).
+// Strided row copy fp32: dst[r*ldd + j] = src[r*lds + j], j < D, r < rows (t2i mask stream concat); row r of a
+// group of rows_per_group is row (r / rpg) * group_stride + r % rpg on either side.  Optionally a second row
+// (dst2 / src2, D2 floats, same row mapping) in the same launch: the row's LayerNorm partials.
 hipError_t rowcopy_launch(float* dst, int ldd, const float* src, int lds, int rows, int D, int rows_per_group,
-                          int dst_group_stride, int src_group_stride, hipStream_t stream);
+                          int dst_group_stride, int src_group_stride, hipStream_t stream, float* dst2 = nullptr,
+                          int ldd2 = 0, const float* src2 = nullptr, int lds2 = 0, int D2 = 0);
 
 }  // namespace pdm
