@@ -34,6 +34,37 @@ def per_kernel(path, counter):
     return {k: (v[0] / v[1], v[1]) for k, v in acc.items()}
 
 
+def roofline_check(src, bench_log):
+    """The bench line's roofline kernel time, recomputed from the kernel trace: the bench times the GEMM launches of
+    the LAST forward of its eager roofline pass (after the timed region; nothing else runs on the GPU after it), so
+    the last `launches_per_forward` GEMM launches of the trace by start time are those launches."""
+    trace = os.path.join(src, "kt", "run_kernel_trace.csv")
+    if not (os.path.exists(trace) and os.path.exists(bench_log)):
+        return None
+    line = [l for l in open(bench_log) if l.startswith("{")]
+    if not line:
+        return None
+    roof = json.loads(line[-1]).get("roofline") or {}
+    n = roof.get("launches_per_forward")
+    if not n:
+        return None
+    rows = []
+    for r in csv.DictReader(open(trace)):
+        name = short(r["Kernel_Name"])
+        if name.startswith("gemm"):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), name))
+    rows.sort()
+    last = rows[-n:]
+    avg_ms = sum(d for _, d, _ in last) / len(last) / 1e6
+    by = defaultdict(list)
+    for _, d, k in last:
+        by[k].append(d)
+    return {"launches": len(last), "avg_launch_ms_rocprof": round(avg_ms, 4),
+            "avg_launch_ms_bench": roof.get("avg_launch_ms"),
+            "per_kernel_avg_ms": {k: round(sum(v) / len(v) / 1e6, 4) for k, v in sorted(by.items())},
+            "note": "the bench's HIP-event average over the same launches (last forward of the eager roofline pass)"}
+
+
 def main():
     tag = sys.argv[1]
     config = sys.argv[2] if len(sys.argv) > 2 else "imagenet256_uvit_large"
@@ -45,6 +76,7 @@ def main():
     kt = os.path.join(src, "kt", "run_kernel_stats.csv")
     if os.path.exists(kt):
         shutil.copy(kt, os.path.join(dst, f"{tag}_{config}_bench_kernel_stats.csv"))
+    roof = roofline_check(src, os.path.join(src, "bench_kt.log"))
     fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     out = {"config": config, "rows": 2 * batch, "precision": precision,
@@ -65,6 +97,8 @@ def main():
             gemm_n += n
     if gemm_n:
         out["gemm_family"] = {"launches": int(gemm_n), "hbm_bytes_per_launch": round((gemm_f + gemm_w) / gemm_n)}
+    if roof:
+        out["roofline_check"] = roof
     json.dump(out, open(os.path.join(dst, f"{tag}_{config}_traffic.json"), "w"), indent=1)
     print(json.dumps(out.get("gemm_family"), indent=1))
 
