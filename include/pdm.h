@@ -194,8 +194,13 @@ typedef struct pdm_gemm_args {
   /* epi = 3 (residual on a bf16 stream): out_bf16 = bf16(A W^T + bias (+ res_in when accumulate)), LayerNorm
    * partials of the rounded values to stats_out; res_in [M][ldri] bf16 may alias out_bf16 */
   const void* res_in; int ldri;
+  /* epi = 2 with accumulate: the fp32 residual is read from res_f32 [M][ldrf] instead of out_f32 (out of place:
+   * out_f32 = res_f32 + A W^T + bias); null = in place */
+  const float* res_f32; int ldrf;
 } pdm_gemm_args;
 int pdm_gemm(const pdm_gemm_args* a, int epi, void* stream);
+/* sizeof(pdm_gemm_args) as compiled into the library (binding layout check) */
+int pdm_gemm_args_size(void);
 /* Implicit-GEMM conv3x3 (stride 1, pad 1) on NHWC bf16 input [B, H>>up, W>>up, Cin] (up = 1: the nearest-x2
  * upsample of libs/autoencoder.py:35-50 folded into the addressing); Wt [N][9*Cin] in (ky, kx, ci) order;
  * output rows = output pixels (b, y, x), N channels (libs/autoencoder.py ResnetBlock conv1/conv2, Upsample.conv) */

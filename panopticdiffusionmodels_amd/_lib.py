@@ -64,10 +64,12 @@ class PdmGemmArgs(ctypes.Structure):
         ("out_scale", ctypes.c_void_p), ("out_scale_ld", ctypes.c_int),
         ("mx_center", ctypes.c_int), ("ln_gcol", ctypes.c_void_p),
         ("res_in", ctypes.c_void_p), ("ldri", ctypes.c_int),
+        ("res_f32", ctypes.c_void_p), ("ldrf", ctypes.c_int),
     ]
 
 
 _SIGS = {
+    "pdm_gemm_args_size": (ctypes.c_int, []),
     "pdm_last_error": (ctypes.c_char_p, []),
     "pdm_version": (ctypes.c_int, []),
     "pdm_device_arch": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
@@ -324,7 +326,7 @@ def mx_quantize_gpu(x):
 
 def gemm_ex(epi, a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=None, accumulate=False,
             ln_stats=None, ln_colsum=None, stats_out=None, out_fp8=None, out_scale=None, eps=1e-5,
-            mx_center=False, ln_gcol=None, res_in=None):
+            mx_center=False, ln_gcol=None, res_in=None, res_f32=None):
     """pdm_gemm with every option (include/pdm.h pdm_gemm_args).  a / w are bf16, or float8_e4m3fn with their
     scale dword arrays (MXFP8)."""
     lib = load()
@@ -356,6 +358,8 @@ def gemm_ex(epi, a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=
     g.ln_gcol = ln_gcol.data_ptr() if ln_gcol is not None else None
     if res_in is not None:
         g.res_in, g.ldri = res_in.data_ptr(), res_in.stride(0)
+    if res_f32 is not None:
+        g.res_f32, g.ldrf = res_f32.data_ptr(), res_f32.stride(0)
     check(lib.pdm_gemm(ctypes.byref(g), epi, stream_ptr(a.device)), "pdm_gemm")
 
 

@@ -1142,10 +1142,13 @@ int pdm_gemm(const pdm_gemm_args* g, int epi, void* stream) {
   a.out_scale = g->out_scale; a.out_scale_ld = g->out_scale_ld;
   a.mx_center = g->mx_center; a.ln_gcol = (const bf16*)g->ln_gcol;
   a.res_in = (const bf16*)g->res_in; a.ldri = g->ldri;
+  a.res_f32 = g->res_f32; a.ldrf = g->ldrf;
   PDM_CHECK(pdm::gemm_check(a, epi));
   PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
   return PDM_OK;
 }
+
+int pdm_gemm_args_size(void) { return (int)sizeof(pdm_gemm_args); }
 
 int pdm_gemm_conv3x3_bf16(const void* in, int B, int H, int W, int Cin, int up, const void* Wt, const float* bias,
                           int N, int epi, void* out_bf16, float* out_f32, int accumulate, void* stream) {

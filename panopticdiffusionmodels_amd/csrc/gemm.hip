@@ -166,7 +166,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p, int tiles
         *reinterpret_cast<bf16x4*>(p.out_bf16 + (size_t)m * p.ldo + n) = to_bf16x4(v[0], v[1], v[2], v[3]);
       } else {
         f32x4* r = reinterpret_cast<f32x4*>(p.out_f32 + (size_t)m * p.ldr + n);
-        if (p.accumulate) v += *r;
+        if (p.accumulate)
+          v += p.res_f32 ? *reinterpret_cast<const f32x4*>(p.res_f32 + (size_t)m * p.ldrf + n) : *r;
         *r = v;
         if (p.out_bf16)
           *reinterpret_cast<bf16x4*>(p.out_bf16 + (size_t)m * p.ldo + n) = to_bf16x4(v[0], v[1], v[2], v[3]);
@@ -486,7 +487,9 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int idx = (g * 4 + i) * 512 + tid;
-            const f32x4* r = reinterpret_cast<const f32x4*>(p.out_f32 + (size_t)(m0 + pass * 128 + (idx >> 5)) * p.ldr + n0 + (idx & 31) * 8);
+            const size_t mr = (size_t)(m0 + pass * 128 + (idx >> 5));
+            const f32x4* r = reinterpret_cast<const f32x4*>(p.res_f32 ? p.res_f32 + mr * p.ldrf : p.out_f32 + mr * p.ldr) +
+                             (n0 + (idx & 31) * 8) / 4;
             r0[i] = r[0];
             r1[i] = r[1];
           }
@@ -532,8 +535,9 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
             f32x4* r = reinterpret_cast<f32x4*>(p.out_f32 + (size_t)m * p.ldr + n);
             f32x4 a = v0[i], b = v1[i];
             if (p.accumulate) {
-              a += r[0];
-              b += r[1];
+              const f32x4* rs = p.res_f32 ? reinterpret_cast<const f32x4*>(p.res_f32 + (size_t)m * p.ldrf + n) : r;
+              a += rs[0];
+              b += rs[1];
             }
             r[0] = a;
             r[1] = b;
@@ -1758,6 +1762,8 @@ const char* gemm_check(const GemmArgs& p, int epi) {
     if (p.N % 8 || p.batch > 1 || p.conv) return "gemm(residual): N % 8 == 0, no batch / conv";
   } else if (epi == EPI_F32) {
     if (!p.out_f32 || (p.ldr % 4)) return "gemm: f32 output missing or ldr not a multiple of 4";
+    if (p.res_f32 && (!p.accumulate || p.ldrf % 4 || ((uintptr_t)p.res_f32 & 15) || p.batch > 1))
+      return "gemm: res_f32 needs accumulate, ldrf % 4 == 0, 16-byte alignment and no batch";
     if (p.out_bf16 && (p.ldo % 4)) return "gemm: ldo not a multiple of 4";
   } else {
     return "gemm: unknown epilogue";
@@ -1956,6 +1962,7 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
       if (b.out_bf16) b.out_bf16 += (size_t)m1 * p.ldo;
       if (b.out_f32) b.out_f32 += (size_t)m1 * p.ldr;
       if (b.res_in) b.res_in += (size_t)m1 * p.ldri;
+      if (b.res_f32) b.res_f32 += (size_t)m1 * p.ldrf;
       if (b.stats_out) b.stats_out += (size_t)m1 * p.stats_ld * 2;
       if (b.ln_stats) b.ln_stats += (size_t)m1 * p.ln_ld * 2;
       const hipError_t e = gemm_launch(a, epi, stream);

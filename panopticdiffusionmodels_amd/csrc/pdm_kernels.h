@@ -68,6 +68,9 @@ struct GemmArgs {
   // EPI_RES residual input [M][ldri] bf16 (may alias out_bf16: each element is read before it is written, by
   // the same thread)
   const bf16* res_in; int ldri;
+  // EPI_F32 with accumulate: the residual is read from res_f32 [M][ldrf] instead of out_f32 (out of place:
+  // out_f32 = res_f32 + A W^T + bias; the training forward keeps every block's input and output streams)
+  const float* res_f32; int ldrf;
   // tuning knobs (set by gemm_launch): raster = row panels per tile group inside an XCD's range (0: row-major);
   // dbg_tile0 = stage every tile's operands from tile (0, 0) (timing experiments only: wrong results)
   int raster, dbg_tile0;

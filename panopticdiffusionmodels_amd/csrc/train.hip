@@ -161,8 +161,10 @@ struct TC {
 };
 
 int t_gemm(const TC& c, const bf16* A, int lda, const bf16* W, const float* bias, int M, int N, int K, int epi, bf16* ob,
-           int ldo, float* of, int ldr, int acc, const bf16* A2 = nullptr, int lda2 = 0, int K1 = 0) {
+           int ldo, float* of, int ldr, int acc, const bf16* A2 = nullptr, int lda2 = 0, int K1 = 0,
+           const float* res = nullptr) {
   pdm::GemmArgs a{};
+  a.res_f32 = res; a.ldrf = res ? ldr : 0;   // out-of-place residual: of = res + A W^T + bias
   a.A1 = A; a.lda1 = lda;
   a.A2 = A2; a.lda2 = lda2; a.K1 = A2 ? K1 : K;
   a.W = W; a.bias = bias;
@@ -246,9 +248,9 @@ int block_fwd(const TC& c, int b, int rows) {
     TR_CHECK(pdm::attention_check(a));
     TR_HIP(pdm::attention_launch(a, c.s));
   }
-  TR_HIP(hipMemcpyAsync(X1, X0, (size_t)M * D * 4, hipMemcpyDeviceToDevice, c.s));
+  // x1 = x0 + proj(attn), out of place (both streams are kept for the LayerNorm backward)
   TR_TRY(t_gemm(c, w.ATT[b], D, t->wb(pre + ".attn.proj.weight"), t->f(pre + ".attn.proj.bias"), M, D, D, pdm::EPI_F32,
-                nullptr, 0, X1, D, 1));
+                nullptr, 0, X1, D, 1, nullptr, 0, 0, X0));
   TR_TRY(t_ln(c, X1, M, t->f(pre + ".norm2.weight"), t->f(pre + ".norm2.bias"), w.H2[b], M, 0, 0));
   TR_TRY(t_gemm(c, w.H2[b], D, t->wb(pre + ".mlp.fc1.weight"), t->f(pre + ".mlp.fc1.bias"), M, Hd, D, pdm::EPI_BF16,
                 w.U[b], Hd, nullptr, 0, 0));
@@ -258,9 +260,8 @@ int block_fwd(const TC& c, int b, int rows) {
   const bool last = b == t->nb - 1;
   float* out = last ? w.XF : (t->skip_block(b + 1) ? w.XTMP : w.X0[b + 1]);
   bf16* outb = b < t->nhalf ? w.SK[b] : (!last && t->skip_block(b + 1) ? w.XS[b + 1] : nullptr);
-  TR_HIP(hipMemcpyAsync(out, X1, (size_t)M * D * 4, hipMemcpyDeviceToDevice, c.s));
   TR_TRY(t_gemm(c, w.Gl[b], Hd, t->wb(pre + ".mlp.fc2.weight"), t->f(pre + ".mlp.fc2.bias"), M, D, Hd, pdm::EPI_F32,
-                outb, D, out, D, 1));
+                outb, D, out, D, 1, nullptr, 0, 0, X1));
   return PDM_OK;
 }
 

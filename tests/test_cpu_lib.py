@@ -24,6 +24,13 @@ def test_lib_exports_header_symbols():
     assert lib.pdm_version() >= 1
 
 
+def test_gemm_args_layout_matches_binding():
+    """The ctypes mirror of pdm_gemm_args has the size the library was compiled with (no field drift)."""
+    import ctypes
+    from panopticdiffusionmodels_amd import _lib
+    assert _lib.load().pdm_gemm_args_size() == ctypes.sizeof(_lib.PdmGemmArgs)
+
+
 def test_create_and_param_table_without_gpu():
     """Handle creation / parameter table / workspace sizing are pure host logic (no GPU call)."""
     import ctypes

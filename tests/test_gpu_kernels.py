@@ -286,6 +286,30 @@ def test_gemm_residual_bf16(lib, algo, M, N, K, mode):
     assert rel(st, _ref_partials(out.float())) < 1e-5
 
 
+@pytest.mark.parametrize("algo", [0, 1, 3, 7])
+@pytest.mark.parametrize("M,N,K", [(4133, 1024, 1024), (515, 1152, 2048), (300, 264, 64)])
+def test_gemm_residual_f32_out_of_place(lib, algo, M, N, K):
+    """fp32 residual read from res_f32 (include/pdm.h pdm_gemm_args.res_f32): out_f32 = res + A W^T + bias, the
+    residual untouched, the optional bf16 copy of the sum; vs fp32 torch (the training forward's x1 = x0 + proj)."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + algo + 11)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    res = torch.randn(M, N, device="cuda", generator=g) * 3 + 2.0
+    res0 = res.clone()
+    out = torch.full((M, N), float("nan"), device="cuda")
+    cp = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
+    try:
+        lib.gemm_ex(lib.EPI_F32, a, w, bias, out=cp, out_f32=out, accumulate=True, res_f32=res)
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+    ref = a.float() @ w.float().t() + bias + res0
+    assert torch.equal(res, res0)
+    assert rel(out, ref) < 2e-3
+    assert torch.equal(cp, out.bfloat16())
+
+
 def test_gemm_bad_shape(lib):
     a = torch.zeros(16, 100, device="cuda", dtype=torch.bfloat16)
     w = torch.zeros(128, 100, device="cuda", dtype=torch.bfloat16)
