@@ -292,10 +292,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs p, const DT* dh) 
     }
   }
   // the block's four waves' partials summed through LDS: one dgamma / dbeta partial row per block
-  // (partials [2][gridDim.x][D]; fewer rows for the column-sum passes that follow)
+  // (partials [gridDim.x][2][D]; fewer rows for the column-sum passes that follow)
   __shared__ f32x4 red[4][2][64];
-  float* pg = p.part + (size_t)blockIdx.x * p.D;                          // dgamma partials [nblk][D]
-  float* pb = p.part + ((size_t)gridDim.x + blockIdx.x) * p.D;            // dbeta partials  [nblk][D]
+  float* pg = p.part + (size_t)blockIdx.x * 2 * p.D;                      // partials [nblk][2][D]: dgamma
+  float* pb = pg + p.D;                                                    //                         dbeta
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     red[wave][0][lane] = dg[i];
@@ -846,15 +846,17 @@ hipError_t ln_bwd_launch(const LnBwdArgs& args, const void* dh, int dh_bf16, flo
 #undef PDM_LNB
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // partials [2][nblk][D] in the first part of the scratch; the column sums use the rest
+  // partials [nblk][2][D] in the first part of the scratch; the column sums use the rest.  When dbeta follows
+  // dgamma in the parameter buffer (the flat layout's norm.weight, norm.bias) one column-sum chain covers both.
   const int nw = nblk;
   float* rest = p.part + (size_t)2 * nw * p.D;
   const size_t rest_bytes = p.part_bytes - (size_t)2 * nw * p.D * 4;
-  if ((e = colsum_launch(p.part, 0, p.D, nw, p.D, 0, 0, 0, dgamma, p.accumulate_params, rest, rest_bytes, stream)) !=
+  if (dbeta == dgamma + p.D)
+    return colsum_launch(p.part, 0, 2 * p.D, nw, 2 * p.D, 0, 0, 0, dgamma, p.accumulate_params, rest, rest_bytes, stream);
+  if ((e = colsum_launch(p.part, 0, 2 * p.D, nw, p.D, 0, 0, 0, dgamma, p.accumulate_params, rest, rest_bytes, stream)) !=
       hipSuccess)
     return e;
-  return colsum_launch(p.part + (size_t)nw * p.D, 0, p.D, nw, p.D, 0, 0, 0, dbeta, p.accumulate_params, rest,
-                       rest_bytes, stream);
+  return colsum_launch(p.part + p.D, 0, 2 * p.D, nw, p.D, 0, 0, 0, dbeta, p.accumulate_params, rest, rest_bytes, stream);
 }
 
 hipError_t gelu_fwd_launch(const bf16* u, bf16* g, long long n, hipStream_t stream) {
