@@ -182,12 +182,22 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p, int tiles_k)
   }
 }
 
-// dst[n * ldc + k] (+)= sum_s part[s][n][k]  (part compact [nparts][N][K]), K % 4 == 0
-__global__ __launch_bounds__(256) void reduce_parts_kernel(const float* part, int nparts, int N, int K, float* dst,
-                                                           int ldc, int accumulate) {
+// dst[n * ldc + k] (+)= sum_s part[s][n][k]  (part compact [nparts][N][K]), K % 4 == 0.  Two such reductions in one
+// launch (the dW partials and the fused bias-gradient partials of one split dW GEMM): blocks [0, nblk_a) take the
+// first, the rest the second.
+struct PartsJob {
+  const float* part; int N, K; float* dst; int ldc, accumulate;
+};
+__global__ __launch_bounds__(256) void reduce_parts_kernel(PartsJob ja, PartsJob jb, int nparts, int nblk_a) {
+  const bool second = (int)blockIdx.x >= nblk_a;
+  const PartsJob& j = second ? jb : ja;
+  const int bid = second ? blockIdx.x - nblk_a : blockIdx.x, nb = second ? gridDim.x - nblk_a : nblk_a;
+  const float* part = j.part;
+  const int N = j.N, K = j.K, ldc = j.ldc, accumulate = j.accumulate;
+  float* dst = j.dst;
   const long long nk4 = (long long)N * (K >> 2);
   const long long NK = (long long)N * K;
-  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < nk4; e += (long long)gridDim.x * 256) {
+  for (long long e = bid * 256ll + threadIdx.x; e < nk4; e += (long long)nb * 256) {
     const int n = (int)(e / (K >> 2)), k = (int)(e - (long long)n * (K >> 2)) * 4;
     f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int i = 0; i < nparts; ++i) s += *reinterpret_cast<const f32x4*>(part + i * NK + (size_t)n * K + k);
@@ -782,11 +792,10 @@ hipError_t wgrad_launch(const WgradArgs& args, float* part, size_t part_bytes, h
     hipLaunchKernelGGL(wgrad_kernel<128>, dim3(tiles, split), dim3(256), 3 * (32 * 128 * 2 * 2), stream, p, tiles_k);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || split == 1) return e;
-  hipLaunchKernelGGL(reduce_parts_kernel, dim3(grid_for(nk / 4)), dim3(256), 0, stream, part, split, p.N, p.K, args.C,
-                     args.ldc, args.accumulate);
-  if ((e = hipGetLastError()) != hipSuccess || !args.bias_out) return e;
-  hipLaunchKernelGGL(reduce_parts_kernel, dim3(grid_for(p.N / 4)), dim3(256), 0, stream, p.bias_out, split, 1, p.N,
-                     args.bias_out, p.N, args.bias_acc);
+  const PartsJob ja{part, p.N, p.K, args.C, args.ldc, args.accumulate};
+  const PartsJob jb{p.bias_out, 1, p.N, args.bias_out, p.N, args.bias_acc};
+  const int ga = (int)grid_for(nk / 4), gb = args.bias_out ? (int)grid_for(p.N / 4) : 0;
+  hipLaunchKernelGGL(reduce_parts_kernel, dim3(ga + gb), dim3(256), 0, stream, ja, jb, split, ga);
   return hipGetLastError();
 }
 
