@@ -55,9 +55,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=50,
-                    help="images per GPU per step (default: the reference's mini_batch_size, "
-                         "configs/imagenet256_uvit_large.py:66)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="images per GPU per step (default: the config's mini_batch_size -- the reference's 50 "
+                         "for ImageNet, configs/imagenet256_uvit_large.py:66; 32 for MSCOCO; BASELINE's 4 for "
+                         "CIFAR-10)")
     ap.add_argument("--config", default="imagenet256_uvit_large")
     ap.add_argument("--lanes", type=int, default=2,
                     help="sample the batch as this many concurrent sub-batches on their own streams (fills the "
@@ -99,7 +100,7 @@ def main():
 
     full = configs.get_config(args.config)
     ncfg = dict(full["nnet"])
-    B = args.batch
+    B = args.batch if args.batch is not None else int(full.get("mini_batch_size", 50))
     # weights: seeded synthetic (no checkpoints offline); identical on every rank
     sd = weights.nnet_state_dict(ncfg, seed=0, init="reference", device=dev)
     net = get_nnet(**ncfg).to(dev).eval()
@@ -133,7 +134,9 @@ def main():
         sampler = ClassCondSampler(net, front_end=full["front_end"], cfg_scale=full["cfg_scale"],
                                    null_label=null_label, steps=full["sample_steps"], eps=full.get("eps"),
                                    use_graph=not args.no_graph, lanes=args.lanes)
-    ae = get_model(None, scale_factor=full.get("scale_factor", 0.18215), seed=1).to(dev) if not args.no_decode else None
+    # configs[0] (CIFAR-10) samples pixels: no autoencoder (eval.py:56-86)
+    decode = full.get("decode", True) and not args.no_decode
+    ae = get_model(None, scale_factor=full.get("scale_factor", 0.18215), seed=1).to(dev) if decode else None
 
     # inputs for every (warmup + timed) step, generated per GLOBAL sample index and resident in HBM
     nsteps = args.warmup + args.steps
@@ -240,11 +243,8 @@ def main():
                    "nfe": sampler.nfe, "hip_graph": not args.no_graph, "parallelism": f"dp{world} (batch-sharded)",
                    "lanes": sampler.lanes},
         "roofline": roof,
-        "end_to_end": None if tf_img is None or ae is None else {
-            "algorithmic_tflop_per_image": tf_img, "achieved_tflops": round(value * tf_img, 1),
-            "frac_of_peak": round(value * tf_img * 1e12 / (world * PEAK_BF16), 4) if precision == "bf16" else None,
-            "roofline_images_per_sec": round(world * PEAK_BF16 / (tf_img * 1e12), 1) if precision == "bf16" else None,
-            "note": "whole job: images/s x algorithmic FLOPs per image (SURVEY.md §8d) vs N x the dense bf16 peak"},
+        "end_to_end": None if tf_img is None or (ae is None and decode_expected(full)) else
+        end_to_end(value, world, tf_img, ncfg, full, precision, sampler.nfe),
         "breakdown_ms_per_step": {"sample_50nfe": round(samp_ms, 2), "decode": round(dec_ms, 2),
                                   "note": "HIP events on the launch stream around each timed step (graph replay)"},
     }
@@ -256,6 +256,32 @@ def main():
         dist.destroy_process_group()
 
 
+def decode_expected(full):
+    return bool(full.get("decode", True))
+
+
+def end_to_end(value, world, tf_img, ncfg, full, precision, nfe):
+    """images/s x algorithmic FLOPs per image against the roofline time of one image: every
+    FLOP at its dense MFMA peak -- bf16, or for the MXFP8 configs[4] the block Linears the precision mode runs in
+    fp8 at the fp8 peak and everything else (skip_linear, fc1 in 'fp8', attention, decode) at the bf16 peak."""
+    peak_s = tf_img * 1e12 / PEAK_BF16
+    note = "whole job: images/s x algorithmic FLOPs per image (SURVEY.md §8d) vs N x the dense bf16 peak"
+    if precision != "bf16":
+        D, depth = ncfg["embed_dim"], ncfg["depth"]
+        Hd = int(D * ncfg.get("mlp_ratio", 4))
+        L = (ncfg["img_size"] // ncfg["patch_size"]) ** 2 + 2
+        lin = {"qkv": 3 * D * D, "proj": D * D, "fc1": D * Hd, "fc2": Hd * D}
+        fp8 = ("qkv", "proj", "fc2") if precision == "fp8" else ("qkv", "proj", "fc1", "fc2")
+        rows_per_img = nfe * (2 if full.get("cfg_scale", 0) > 0 else 1)
+        f8 = rows_per_img * (depth + 1) * 2.0 * L * sum(lin[k] for k in fp8)
+        peak_s = (tf_img * 1e12 - f8) / PEAK_BF16 + f8 / PEAK_FP8
+        note = (f"whole job vs the FLOP-weighted dense peak: {f8 / 1e12:.2f} of {tf_img} TF per image "
+                f"({'/'.join(fp8)}) at the MXFP8 peak, the rest at bf16")
+    return {"algorithmic_tflop_per_image": tf_img, "achieved_tflops": round(value * tf_img, 1),
+            "frac_of_peak": round(value * peak_s / world, 4),
+            "roofline_images_per_sec": round(world / peak_s, 1), "note": note}
+
+
 def metric_name(config, zshape, with_decode):
     """BASELINE.json's metric for the headline config; the same wording with the model / resolution of the
     other configs (their lines are extra evidence, not the headline)."""
@@ -263,7 +289,10 @@ def metric_name(config, zshape, with_decode):
         return "images/sec (whole node), ImageNet256 U-ViT-L 50-step DPM-Solver, 1/2/4/8 GPU"
     data = {"imagenet256_uvit_huge": "ImageNet256", "imagenet512_uvit_huge": "ImageNet512",
             "mscoco_uvit_small": "MSCOCO256 t2i + panoptic", "cifar10_uvit_small": "CIFAR10"}.get(config, config)
-    res = 8 * zshape[-1] if config != "cifar10_uvit_small" else zshape[-1]
+    if config == "cifar10_uvit_small":   # pixel-space net: the sample IS the image (eval.py:56-86)
+        return (f"images/sec (whole node), {data} {MODEL_NAMES.get(config, config)} 50-step DPM-Solver, "
+                f"{zshape[-1]}x{zshape[-1]} pixels (no decoder)")
+    res = 8 * zshape[-1]
     return (f"images/sec (whole node), {data} {MODEL_NAMES.get(config, config)} 50-step DPM-Solver"
             f"{f', {res}x{res} decode' if with_decode else ', latents only (no decode)'}")
 
@@ -374,11 +403,12 @@ def cpu_baseline(full, ncfg, with_decode):
     sd = weights.nnet_state_dict(ncfg, seed=0, init="reference")
     if ncfg["name"] == "uvit_t2i":
         return cpu_baseline_t2i(full, ncfg, kw, sd, cores, with_decode)
-    B = 2
+    # configs[0] (CIFAR-10, unconditional, no CFG): BASELINE's batch of 4; the latent configs: 2 images
+    B = 4 if ncfg.get("num_classes", -1) <= 0 else 2
     g = torch.Generator().manual_seed(0)
     z = torch.randn(B, *full["z_shape"], generator=g)
-    null = ncfg["num_classes"] - 1
-    y = torch.randint(0, null, (B,), generator=g)
+    null = ncfg["num_classes"] - 1 if ncfg.get("num_classes", -1) > 0 else None
+    y = torch.randint(0, null, (B,), generator=g) if null is not None else None
 
     def nnet(x, t, yy):
         return uvit_ref.uvit_forward(sd, kw, x, t, yy)
@@ -410,9 +440,12 @@ def cpu_baseline(full, ncfg, with_decode):
     assert torch.isfinite(lat).all()
     return {"value": round(B / (t_sample + t_dec), 5), "unit": "images/sec", "cores": cores, "kind": "port",
             "cpu": cpu_model(),
-            "sample": f"one full {nfe[0]}-NFE {full['front_end']} sample of B={B} images (CFG {full['cfg_scale']}: "
-                      f"cond + uncond forwards of {B} rows per NFE) = {t_sample:.1f} s, + KL-f8 decode of {B} "
-                      f"images = {t_dec:.1f} s; images/sec = {B} / total"}
+            "sample": f"one full {nfe[0]}-NFE {full['front_end']} sample of B={B} images ("
+                      + (f"CFG {full['cfg_scale']}: cond + uncond forwards of {B} rows per NFE"
+                         if full["cfg_scale"] > 0 else f"no guidance: one forward of {B} rows per NFE")
+                      + f") = {t_sample:.1f} s"
+                      + (f", + KL-f8 decode of {B} images = {t_dec:.1f} s" if with_decode else ", no decode (pixels)")
+                      + f"; images/sec = {B} / total"}
 
 
 if __name__ == "__main__":

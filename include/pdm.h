@@ -80,9 +80,11 @@ typedef struct pdm_uvit_cfg {
    * Supported: 0 / 0xF, and 0xB (mlp.fc1 in bf16: the forward error of the H/4 net drops from 6.9e-2 to
    * 5.0e-2 rel-L2, tools/fp8_ablation.py).  A bf16 Linear's weight is registered as in the bf16 path. */
   int fp8_linears;
-  /* residual stream precision between blocks.  0 (default): bf16, as the reference's own GPU run keeps it under
-   * autocast (each Linear output is added to x in the autocast dtype); 1: fp32.  The t2i and MXFP8 forwards
-   * always keep it fp32. */
+  /* residual stream precision between blocks, for every forward (class-conditional, t2i, MXFP8).  0 (default):
+   * bf16 -- a performance choice, NOT the reference's numerics: under autocast the reference's x stays fp32
+   * through the in-blocks and the mid-block (x + pos_embed promotes it, libs/uvit.py:212) and is half precision
+   * (fp16) only after each out-block's skip_linear; 1: fp32 throughout (closer to the reference: L/2 forward
+   * 5.7e-3 vs 7.5e-3 rel-L2 to the fp32 oracle). */
   int residual_fp32;
 } pdm_uvit_cfg;
 

@@ -42,10 +42,27 @@ def build_plan(front_end, steps=50, eps=None, betas=None):
 
 def _drop_stale_graph(st, nnet):
     """A captured graph holds the device addresses of the net's packed weights and workspace.  Anything that
-    rebuilds the native handle (load_state_dict, .to(), set_precision) frees those, so the graph is dropped and
-    recaptured on the new handle rather than replayed on freed memory."""
-    if st["graph"] is not None and st.get("generation") != nnet.generation:
+    rebuilds the native handle (load_state_dict, .to(), set_precision, set_residual) frees those, so the graph is
+    dropped and recaptured on the new handle rather than replayed on freed memory; a lane's private workspace is
+    re-sized for the new handle (an fp8 or fp32-residual handle needs more than the one it was sized for)."""
+    handle = nnet.native()   # (re)builds the handle first, so `generation` names the one the loop will use
+    if st.get("generation") != nnet.generation:
         st["graph"] = None
+        if st.get("ws") is not None:
+            need = handle.workspace_bytes(st["rows"])
+            if st["ws"].numel() < need:
+                st["ws"] = None
+                st["ws"] = torch.empty(need, dtype=torch.uint8, device=st["xin"].device)
+        st["generation"] = nnet.generation
+
+
+def _lane_streams(owner, main):
+    """Streams of the concurrent lanes: lane 0 runs on the caller's stream, lanes 1.. on streams of their own.
+    Under HIP's default of 4 hardware queues per process (GPU_MAX_HW_QUEUES) every extra stream competes with the
+    launch stream and RCCL's for a queue, so one fewer keeps the lanes concurrent under torchrun / accelerate."""
+    while len(owner._streams) < owner.lanes - 1:
+        owner._streams.append(torch.cuda.Stream(device=main.device))
+    return [main] + owner._streams[:owner.lanes - 1]
 
 
 class ClassCondSampler:
@@ -82,7 +99,7 @@ class ClassCondSampler:
             # a lane's private workspace (concurrent lanes must not share the handle's)
             ws=None if lane is None else torch.empty(n.native().workspace_bytes(rows), dtype=torch.uint8,
                                                      device=device),
-            rows=rows,
+            rows=rows, generation=n.generation,
             xin=torch.empty(rows, *shp, device=device),           # batched model input [cond | uncond]
             pre=torch.empty(rows, *shp, device=device),           # model output before the final conv
             x=torch.empty(B, *shp, device=device),                # solver state at the step start
@@ -129,19 +146,18 @@ class ClassCondSampler:
 
     def _sample_lanes(self, z, y):
         main = torch.cuda.current_stream(z.device)
-        while len(self._streams) < self.lanes:
-            self._streams.append(torch.cuda.Stream(device=z.device))
+        streams = _lane_streams(self, main)
+        for s in streams[1:]:
+            s.wait_stream(main)   # before lane 0's work is queued on main
         bounds = [round(i * z.shape[0] / self.lanes) for i in range(self.lanes + 1)]
         outs = []
-        for i in range(self.lanes):
-            s = self._streams[i]
-            s.wait_stream(main)
+        for i, s in enumerate(streams):
             with torch.cuda.stream(s):
                 zi = z[bounds[i]:bounds[i + 1]]
                 yi = y[bounds[i]:bounds[i + 1]] if y is not None else None
                 outs.append(self._sample_one(zi, yi, False, lane=i))
-        for i, o in enumerate(outs):
-            main.wait_stream(self._streams[i])
+        for s, o in zip(streams[1:], outs[1:]):
+            main.wait_stream(s)
             o.record_stream(main)
         return torch.cat(outs)
 
@@ -173,7 +189,7 @@ class ClassCondSampler:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._loop(st, B)
-            st["graph"], st["generation"] = g, self.nnet.generation
+            st["graph"] = g
         st["graph"].replay()
         return st["x"].clone()
 
@@ -209,6 +225,7 @@ class T2ISampler:
         st = dict(
             ws=None if lane is None else torch.empty(n.native().workspace_bytes(rows), dtype=torch.uint8,
                                                      device=device),
+            rows=rows, generation=n.generation,
             xin=torch.empty(rows, *shp, device=device), pre=torch.empty(rows, *shp, device=device),
             x=torch.empty(B, *shp, device=device), m=[torch.empty(B, *shp, device=device) for _ in range(3)],
             min=torch.empty(rows, *mshp, device=device), mpre=torch.empty(rows, *mshp, device=device),
@@ -255,18 +272,17 @@ class T2ISampler:
         B = z.shape[0]
         if self.lanes > 1 and B >= self.lanes and self.use_graph:
             main = torch.cuda.current_stream(z.device)
-            while len(self._streams) < self.lanes:
-                self._streams.append(torch.cuda.Stream(device=z.device))
+            streams = _lane_streams(self, main)
+            for s in streams[1:]:
+                s.wait_stream(main)
             bounds = [round(i * B / self.lanes) for i in range(self.lanes + 1)]
             outs = []
-            for i in range(self.lanes):
-                s = self._streams[i]
-                s.wait_stream(main)
+            for i, s in enumerate(streams):
                 lo, hi = bounds[i], bounds[i + 1]
                 with torch.cuda.stream(s):
                     outs.append(self._sample_one(z[lo:hi], context[lo:hi], empty_context, mask_token[lo:hi], i))
-            for i, (a, b) in enumerate(outs):
-                main.wait_stream(self._streams[i])
+            for s, (a, b) in zip(streams[1:], outs[1:]):
+                main.wait_stream(s)
                 a.record_stream(main)
                 b.record_stream(main)
             return torch.cat([a for a, _ in outs]), torch.cat([b for _, b in outs])
@@ -298,6 +314,6 @@ class T2ISampler:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self._loop(st, B)
-                st["graph"], st["generation"] = g, self.nnet.generation
+                st["graph"] = g
             st["graph"].replay()
         return st["x"].clone(), st["pm"][0].clone()

@@ -203,6 +203,15 @@ class HipTrainState:
         target = target.to(self.device, torch.float32).contiguous()
         t_in = t_in.to(self.device, torch.float32).contiguous().reshape(B)
         if y is not None:
+            # the reference's nn.Embedding raises IndexError on an out-of-range label; the kernels would read the
+            # neighbouring parameter (pos_embed) as the embedding and scatter its gradient there, so check here
+            nc = int(self.kw.get("num_classes", -1))
+            if nc <= 0:
+                raise ValueError("HipTrainState: labels given to an unconditional U-ViT (num_classes <= 0)")
+            if y.numel():
+                lo, hi = (int(v) for v in torch.stack([y.min(), y.max()]).cpu())
+                if lo < 0 or hi >= nc:
+                    raise IndexError(f"HipTrainState: label out of range [0, {nc}): min {lo}, max {hi}")
             y = y.to(self.device, torch.int64).contiguous()
         gs = float(1.0 / B if gscale is None else gscale)
         loss = torch.empty(B, dtype=torch.float32, device=self.device)
@@ -240,7 +249,8 @@ class HipTrainState:
             average_gradients(self.G)
 
     def optimizer_step(self):
-        """AdamW at the current scheduled LR, then the EMA update; advances the step counter."""
+        """AdamW at the current scheduled LR, then the EMA update; advances the step counter.  Returns the LR this
+        step applied (train_step reports the next one, as the reference logs it)."""
         o = self.optimizer
         lr = customized_lr(o["lr"], self.step, self.lr_scheduler.get("warmup_steps", -1))
         b1, b2 = o["betas"]
@@ -251,6 +261,10 @@ class HipTrainState:
                    "pdm_train_adamw")
         self.step += 1
         return lr
+
+    def current_lr(self):
+        """The rate the next optimizer_step applies (optimizer.param_groups[0]['lr'] after lr_scheduler.step())."""
+        return customized_lr(self.optimizer["lr"], self.step, self.lr_scheduler.get("warmup_steps", -1))
 
     def train_step(self, x0, y=None, objective="discrete", schedule=None, sde=None, rng=None):
         """One iteration of train_ldm_discrete.py:159-175 (objective 'discrete', Schedule) or train_ldm.py
@@ -265,12 +279,14 @@ class HipTrainState:
         else:
             raise NotImplementedError(objective)
         self.all_reduce_grads()
-        lr = self.optimizer_step()
+        self.optimizer_step()
         m = loss.mean()
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             dist.all_reduce(m, op=dist.ReduceOp.SUM)
             m /= dist.get_world_size()
-        return dict(loss=m, lr=lr)
+        # the reference returns optimizer.param_groups[0]['lr'] read after lr_scheduler.step()
+        # (train_ldm_discrete.py:174-177): the rate of the NEXT step
+        return dict(loss=m, lr=self.current_lr())
 
 
 def average_gradients(g):

@@ -13,7 +13,9 @@ make_golden._inputs), so only outputs and checksums are stored:
   sample/<config>/*   a full 50-NFE CFG sample of one image through the reference solver front end the config
                       names (eval_ldm.py:66-108 for dpm_solver_pytorch, eval_ldm_discrete.py:72-102 for
                       dpm_solver_pp, train_t2i_discrete.py:387-546 for the panoptic t2i), weights init="reference"
-                      seed 0 (the bench nets), z_T / labels / contexts from parallel.sample_inputs-style seeds
+                      seed 0 (the bench nets), z_T / labels / contexts from parallel.sample_inputs-style seeds;
+                      CIFAR-10 (configs[0]): 4 images, unconditional, no CFG, pixel space, eval.py:47-86
+                      (ScoreModel(nnet, 'noise_pred', VPSDE) -> dpm_solver_pytorch model_wrapper, time_input_type '0')
 Nothing here is imported by the product or run on the GPU box; the .npz is data.
 """
 import os
@@ -28,16 +30,19 @@ from make_golden import C, W, _import_reference, _inputs, _np, _sd_checksum  # n
 
 CONFIGS = ["cifar10_uvit_small", "imagenet256_uvit_large", "imagenet256_uvit_huge", "imagenet512_uvit_huge",
            "mscoco_uvit_small"]
-SAMPLE_CONFIGS = ["imagenet256_uvit_large", "imagenet256_uvit_huge", "imagenet512_uvit_huge", "mscoco_uvit_small"]
+SAMPLE_CONFIGS = ["cifar10_uvit_small", "imagenet256_uvit_large", "imagenet256_uvit_huge", "imagenet512_uvit_huge",
+                  "mscoco_uvit_small"]
 BETAS = (torch.linspace(0.00085 ** 0.5, 0.0120 ** 0.5, 1000, dtype=torch.float64) ** 2).numpy()
 
 
 def sample_inputs(name, seed=99):
-    """One image's sampling inputs: z_T, label (class-conditional), context / empty context / mask token (t2i)."""
+    """One image's sampling inputs: z_T, label (class-conditional), context / empty context / mask token (t2i).
+    configs[0] (CIFAR-10, pixel space, no CFG) samples the BASELINE batch of 4 images."""
     full = C.get_config(name)
     n = full["nnet"]
     g = torch.Generator().manual_seed(seed)
-    out = {"z": torch.randn(1, *full["z_shape"], generator=g)}
+    nb = 4 if name == "cifar10_uvit_small" else 1
+    out = {"z": torch.randn(nb, *full["z_shape"], generator=g)}
     if n.get("num_classes", -1) > 0:
         out["y"] = torch.randint(0, n["num_classes"] - 1, (1,), generator=g)
     if n["name"] == "uvit_t2i":
@@ -110,6 +115,12 @@ def gen_sample(mods, out, names=SAMPLE_CONFIGS):
                     return c + scale * (c - u), None
                 z, _ = pp.DPM_Solver(model_fn, ns, predict_x0=True, thresholding=False).sample(
                     inp["z"].clone(), steps=50, eps=1.0 / 1000, T=1.0)
+            elif not (scale and scale > 0):   # eval.py:47-49, 56-86: unconditional, no CFG, pixel space
+                score = sde.ScoreModel(net, pred="noise_pred", sde=sde.VPSDE())
+                ns = dpt.NoiseScheduleVP(schedule="linear")
+                mf = dpt.model_wrapper(score.noise_pred, ns, time_input_type="0", model_kwargs=dict())
+                z = dpt.DPM_Solver(mf, ns).sample(inp["z"].clone(), steps=50, eps=1e-4,
+                                                  adaptive_step_size=False, fast_version=True)
             else:   # eval_ldm.py:66-108
                 null = full["nnet"]["num_classes"] - 1
 

@@ -21,7 +21,7 @@ from panopticdiffusionmodels_amd import weights as W
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FWD = ["cifar10_uvit_small", "imagenet256_uvit_large", "imagenet256_uvit_huge", "imagenet512_uvit_huge",
        "mscoco_uvit_small"]
-SAMPLE = ["imagenet256_uvit_large", "imagenet256_uvit_huge", "imagenet512_uvit_huge", "mscoco_uvit_small"]
+SAMPLE = ["cifar10_uvit_small", "imagenet256_uvit_large", "imagenet256_uvit_huge", "imagenet512_uvit_huge", "mscoco_uvit_small"]
 TOL_SAMPLE = {"bf16": 1e-2, "fp8": 3e-2}   # final latent after 50 NFE vs the reference
 
 
@@ -58,11 +58,12 @@ def fwd_inputs(name, B=2, seed=5):
 
 
 def sample_inputs(name, seed=99):
-    """= make_fullsize_golden.sample_inputs."""
+    """= make_fullsize_golden.sample_inputs (configs[0], CIFAR-10: the BASELINE batch of 4 images)."""
     full = C.get_config(name)
     n = full["nnet"]
     g = torch.Generator().manual_seed(seed)
-    out = {"z": torch.randn(1, *full["z_shape"], generator=g)}
+    nb = 4 if name == "cifar10_uvit_small" else 1
+    out = {"z": torch.randn(nb, *full["z_shape"], generator=g)}
     if n.get("num_classes", -1) > 0:
         out["y"] = torch.randint(0, n["num_classes"] - 1, (1,), generator=g)
     if n["name"] == "uvit_t2i":
@@ -70,6 +71,10 @@ def sample_inputs(name, seed=99):
         out["empty_context"] = torch.randn(n["num_clip_token"], n["clip_dim"], generator=g)
         out["mask_token"] = torch.randn(1, n["num_panoptic_class"], *full["z_shape"][1:], generator=g)
     return out
+
+
+def cfg_scale_zero(full):
+    return not (full.get("cfg_scale") or 0) > 0
 
 
 def _sd(name, seed, init):
@@ -95,6 +100,23 @@ def test_oracle_vs_reference_fullsize_forward(fs, name):
         else:
             eps = uvit_ref.uvit_forward(sd, kw, inp["x"], inp["t"], inp.get("y"))
     assert rel(eps, fs[f"fwd/{name}/eps"]) < 1e-5
+
+
+def test_oracle_vs_reference_cifar_sample(fs):
+    """configs[0] (eval.py:47-86): CIFAR-10 U-ViT-S/2, pixel space, unconditional, no CFG, 50-NFE
+    dpm_solver_pytorch (ScoreModel noise_pred, time fed as t * 999) -- the oracle's trajectory (solver_ref +
+    uvit_ref) against the reference's own final sample of 4 images."""
+    from oracle import solver_ref
+    torch.set_num_threads(min(8, os.cpu_count() or 8))
+    name = "cifar10_uvit_small"
+    cfg, sd = _sd(name, 0, "reference")
+    np.testing.assert_allclose(_checksum(sd), fs[f"sample/{name}/sd_checksum"], rtol=1e-9)
+    kw = dict(cfg)
+    kw.pop("name")
+    fn = solver_ref.cfg_class_closure(lambda x, t, y: uvit_ref.uvit_forward(sd, kw, x, t, y), None, 0.0, None, 999.0)
+    with torch.no_grad():
+        z = solver_ref.pytorch_sample(fn, sample_inputs(name)["z"].clone(), steps=50, eps=1e-4)
+    assert rel(z, fs[f"sample/{name}/z"]) < 1e-5, rel(z, fs[f"sample/{name}/z"])
 
 
 @pytest.fixture(scope="module")
@@ -151,7 +173,9 @@ def test_hip_sampler_vs_reference_fullsize(fs, dev, name, precision):
     else:
         s = ClassCondSampler(net, front_end=full["front_end"], cfg_scale=full["cfg_scale"],
                              null_label=cfg["num_classes"] - 1, steps=50, eps=full.get("eps"))
-        z = s.sample(inp["z"], inp["y"])
+        z = s.sample(inp["z"], inp.get("y"))   # configs[0]: unconditional, cfg_scale 0 (one B-row forward per NFE)
+        if cfg_scale_zero(full):
+            assert not s.cfg and s.nfe == 50
     assert torch.isfinite(z).all()
     err = rel(z, fs[f"sample/{name}/z"])
     print(f"{name} {precision}: final latent rel-L2 vs the reference = {err:.3e}")

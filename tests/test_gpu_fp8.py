@@ -291,3 +291,27 @@ def test_fp8_sampler_vs_bf16(lib):
     err = rel(a, z16)
     print(f"fp8 vs bf16 final latent rel-L2 {err:.3e}")
     assert err < TOL_FP8_FINAL, err
+
+
+def test_fp8_lanes_recapture_after_precision_switch(lib):
+    """Two concurrent lanes (private workspaces sized for the bf16 handle) keep working after set_precision('fp8')
+    rebuilds the handle with a larger workspace: the lanes' workspaces are re-sized and the graphs recaptured; the
+    result matches the single-lane fp8 sampler."""
+    from panopticdiffusionmodels_amd import configs as C
+    from panopticdiffusionmodels_amd.sampler import ClassCondSampler
+    net, _, _ = _huge("imagenet512_uvit_huge", 0, "reference")
+    full = C.get_config("imagenet512_uvit_huge")
+    g = torch.Generator().manual_seed(77)
+    z = torch.randn(4, 4, 64, 64, generator=g).cuda()
+    y = torch.randint(0, 1000, (4,), generator=g).cuda()
+    mk = lambda lanes: ClassCondSampler(net, front_end="dpm_solver_pp", cfg_scale=full["cfg_scale"],  # noqa: E731
+                                        null_label=1000, steps=10, lanes=lanes)
+    net.set_precision("bf16")
+    s2 = mk(2)
+    b16 = s2.sample(z, y)
+    assert torch.isfinite(b16).all()
+    net.set_precision(full["precision"])
+    a = s2.sample(z, y)
+    b = mk(1).sample(z, y)
+    assert torch.isfinite(a).all()
+    assert rel(a, b) < 1e-5, rel(a, b)

@@ -233,3 +233,21 @@ def test_train_lanes_equal_single():
     num = sum(float((p2[k].double() - p1[k].double()).norm() ** 2) for k in p1)
     den = sum(float((p1[k].double() - sd[k].double().to(p1[k].device)).norm() ** 2) for k in p1)
     assert (num / den) ** 0.5 < 0.05
+
+
+def test_train_label_out_of_range_raises():
+    """An out-of-range label raises IndexError (the reference's nn.Embedding does) instead of reading the
+    neighbouring parameter as the embedding; train_step reports the NEXT step's LR as the reference logs it
+    (optimizer.param_groups[0]['lr'] after lr_scheduler.step(), train_ldm_discrete.py:174-177)."""
+    full, kw, sd, st = _state("tiny_uvit_train")
+    nc = kw["num_classes"]
+    g = torch.Generator().manual_seed(5)
+    xt = torch.randn(2, 4, 16, 16, generator=g)
+    t = torch.rand(2, generator=g) * 999
+    eps = torch.randn(2, 4, 16, 16, generator=g)
+    for bad in (nc, -1):
+        with pytest.raises(IndexError):
+            st.forward_backward(xt, t, torch.tensor([0, bad]), eps)
+    st.lr_scheduler["warmup_steps"] = 4
+    out = st.train_step(torch.randn(2, 4, 16, 16, generator=g), torch.tensor([1, nc - 1]))
+    assert st.step == 1 and abs(out["lr"] - st.optimizer["lr"] * 0.25) < 1e-15
