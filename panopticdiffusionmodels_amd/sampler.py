@@ -11,6 +11,8 @@ each a separate PyTorch launch, plus host syncs inside the discrete schedule.  H
 with every coefficient precomputed on the host (solver_core).  Nothing in the loop synchronises with the
 host, so the 50-NFE loop for a fixed batch is captured once into a HIP graph and replayed.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -56,12 +58,17 @@ def _drop_stale_graph(st, nnet):
         st["generation"] = nnet.generation
 
 
+# Priority of the lanes' own streams.  HIP keeps one pool of hardware queues per stream priority, each capped at
+# GPU_MAX_HW_QUEUES (4 by default): a normal-priority lane stream shares a queue with the caller's stream or RCCL's
+# once the process has made a few streams (torchrun / accelerate), and the lanes then run one after the other.
+LANE_STREAM_PRIORITY = int(os.environ.get("PDM_LANE_PRIORITY", "-1"))
+
+
 def _lane_streams(owner, main):
-    """Streams of the concurrent lanes: lane 0 runs on the caller's stream, lanes 1.. on streams of their own.
-    Under HIP's default of 4 hardware queues per process (GPU_MAX_HW_QUEUES) every extra stream competes with the
-    launch stream and RCCL's for a queue, so one fewer keeps the lanes concurrent under torchrun / accelerate."""
+    """Streams of the concurrent lanes: lane 0 runs on the caller's stream, lanes 1.. on streams of their own
+    (LANE_STREAM_PRIORITY), so a lane never waits behind another lane's kernels in a shared hardware queue."""
     while len(owner._streams) < owner.lanes - 1:
-        owner._streams.append(torch.cuda.Stream(device=main.device))
+        owner._streams.append(torch.cuda.Stream(device=main.device, priority=LANE_STREAM_PRIORITY))
     return [main] + owner._streams[:owner.lanes - 1]
 
 

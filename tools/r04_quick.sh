@@ -15,4 +15,6 @@ PDM_KEEP_HW_QUEUES=1 GPU_MAX_HW_QUEUES=4 timeout -k 10 400 python3 -m torch.dist
   --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 1 --steps 3 --warmup 1 \
   --cpu-baseline off > $OUT/torchrun_q4.log 2>&1
 s=$?; tail -2 $OUT/torchrun_q4.log | cut -c1-400; stop_on_fault $s
+timeout -k 10 300 python3 tools/sol_forward.py imagenet256_uvit_large 100 5 > $OUT/sol_l2.log 2>&1
+s=$?; cat $OUT/sol_l2.log; stop_on_fault $s
 echo done
