@@ -42,13 +42,15 @@ int pdm_device_arch(char* buf, int len);
 /* Tile-policy overrides for A/B measurement (0 = automatic; the default everywhere).
  *   GEMM: 1 = 128x128, 2 = 256x256 BK32 ring, 3 = 256x256 BK64 ring, 4 = 256x256 8-phase staggered,
  *         5 / 6 / 7 = 256x256 LDS-DMA descriptor kernel (schedules 0 / 1 / 2; 7 is the automatic choice for
- *         N >= 256), 8 = its 256x128 half-N tile, 9 = a 512x128 tall tile (both N <= 128, bf16 / fp32 epilogues)
+ *         N >= 256 where 11 does not apply), 8 = its 256x128 half-N tile, 9 = a 512x128 tall tile (both N <= 128,
+ *         bf16 / fp32 epilogues), 11 = the persistent 256x256 kernel (schedule 2 run across tiles; bf16 / GELU /
+ *         bf16-residual epilogues, K >= 256: the automatic choice where it applies, else 7)
  *   attention: 1 = streamed K/V per 64-query block, 2 / 3 = head-resident K/V with 2 / 3 query tiles per wave,
  *              4 = head-resident v2 (Dh 64), 7 = head-resident Dh 72 (64 + 8 split); 5/6, 8/9 = their load-only /
  *              math-only timing variants (wrong results) */
 /* GEMM tile-order knob: raster = row panels per tile group inside an XCD's tile range (0 = row-major);
  * dbg_tile0 bit 0 stages every tile's operands from tile (0, 0); bit 1 lets a bf16 GEMM run with no output (mainloop +
- * LDS staging only) -- timing experiments, results are wrong */
+ * LDS staging only); bit 4 skips every 256-tile epilogue -- timing experiments, results are wrong */
 int pdm_set_gemm_tuning(int raster, int dbg_tile0);
 int pdm_set_gemm_algo(int algo);
 int pdm_set_attention_algo(int algo);

@@ -326,15 +326,19 @@ def mx_quantize_gpu(x):
 
 def gemm_ex(epi, a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=None, accumulate=False,
             ln_stats=None, ln_colsum=None, stats_out=None, out_fp8=None, out_scale=None, eps=1e-5,
-            mx_center=False, ln_gcol=None, res_in=None, res_f32=None):
+            mx_center=False, ln_gcol=None, res_in=None, res_f32=None, a2=None):
     """pdm_gemm with every option (include/pdm.h pdm_gemm_args).  a / w are bf16, or float8_e4m3fn with their
-    scale dword arrays (MXFP8)."""
+    scale dword arrays (MXFP8); a2 (bf16) continues a along K (the split-K skip_linear operand)."""
     lib = load()
     require_gpu(a)
     M, K = a.shape
     N = w.shape[0]
     g = PdmGemmArgs()
     g.A1, g.lda1 = a.data_ptr(), a.stride(0)
+    g.K1 = K
+    if a2 is not None:
+        g.A2, g.lda2 = a2.data_ptr(), a2.stride(0)
+        K = K + a2.shape[1]
     g.W, g.ldw = w.data_ptr(), w.stride(0)
     g.bias = bias.data_ptr() if bias is not None else None
     g.M, g.N, g.K = M, N, K

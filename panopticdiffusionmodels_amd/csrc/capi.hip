@@ -735,7 +735,8 @@ const char* pdm_last_error(void) { return g_err.c_str(); }
 int pdm_version(void) { return 1; }
 
 int pdm_set_gemm_algo(int algo) {
-  if (algo < 0 || algo > 9) return fail(PDM_ERR_ARG, "pdm_set_gemm_algo: algo must be 0 (auto) or 1..9");
+  if (algo < 0 || algo > 11 || algo == 10)
+    return fail(PDM_ERR_ARG, "pdm_set_gemm_algo: algo must be 0 (auto), 1..9 or 11");
   pdm::gemm_set_algo(algo);
   return PDM_OK;
 }

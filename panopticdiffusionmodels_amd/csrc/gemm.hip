@@ -1212,6 +1212,523 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
 }
 
 // ------------------------------------------------------------------------------------------------
+// Persistent 256 x 256 kernel (algo 11, the default for the U-ViT block GEMMs: bf16 / GELU outputs with or
+// without the fused-LayerNorm consumer, and the bf16 residual epilogue with its LayerNorm partials).
+//
+// gemm8d's main loop (SCHED 2) runs unchanged, but a workgroup owns one CU for the whole launch and walks its
+// XCD's tile range in a static round robin, and the LDS-DMA ring runs on across tile boundaries: the K-tiles are
+// numbered continuously over the workgroup's tiles (ring slot = global K-tile & 1), so the last K-tile's phases
+// already issue the next tile's K-tile 0 and the A0 W0 W1 halves of its K-tile 1 exactly as they would issue
+// K-tiles of the same tile.  The next tile's main loop therefore starts on landed operands instead of an empty
+// pipeline.  That needs an epilogue that leaves the ring alone, so nothing is staged through LDS:
+//  * bf16 / GELU: the accumulator fragment holds 4 consecutive columns of one row per lane; two fragments 16
+//    columns apart are converted to bf16 and exchanged between the lane rows {0,1} and {2,3} with
+//    v_permlane16_swap, after which every lane holds 8 consecutive columns (16 bytes) of its row and stores them
+//    with one buffer store (16 rows x 64 B per instruction);
+//  * residual: the bf16 residual is loaded in that 16-byte layout (buffer loads, zeros out of range), swapped
+//    back into the fragment layout, added in fp32 (acc + bias + residual, rounded once, as EPI_RES), and the
+//    LayerNorm partials (sum, M2 about the 256-column group mean) of the rounded rows are reduced per wave
+//    (permlane swaps across the 4 lane rows holding a row's columns) and across the 4 column waves in LDS.
+// Small per-tile tables (the LN consumer's raw row partials, bias, LN column sums) are LDS-DMA'd for the next
+// tile while the current epilogue runs.  Every store is a buffer store with out-of-range offsets dropped, so a
+// lane issues the same number of VMEM ops on every tile; the first K-tile after an epilogue waits with the
+// epilogue's E stores excluded from the count (they retire one phase later), so the stores overlap the next
+// tile's first MFMAs.
+constexpr int S_RING = 2 * 4 * 128 * 128;      // 128 KiB ring (as gemm8d)
+constexpr int S_RAW = S_RING;                  // raw LN partials of a tile's 256 rows: 256 x ln_ld float2 (<= 16 KiB)
+constexpr int S_LNROW = S_RAW + 256 * 8 * 8;   // merged (mean, rstd) per row (2 KiB)
+constexpr int S_COL = S_LNROW + 256 * 8;       // bias [256] | LN colsum [256] (2 KiB)
+constexpr int S_STAT = S_COL + 2 * 256 * 4;    // residual epilogue: per (row, column wave) sum / M2 (8 KiB)
+constexpr int S_SMEM = S_STAT + 256 * 4 * 8;   // 156 KiB
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_n() {   // s_waitcnt vmcnt(N), N < 64
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  bf16x2 r;
+  r[0] = (bf16)a;
+  r[1] = (bf16)b;
+  return __builtin_bit_cast(unsigned, r);
+}
+__device__ __forceinline__ float bf16lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+
+// sum over the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 (the four 16-lane rows of one fragment column), in every lane
+__device__ __forceinline__ float xrow_sum4(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// LDS accesses the compiler does not see: hipcc drains vmcnt before a visible LDS access while an LDS-DMA may be
+// pending, which would wait for the epilogue's stores and the next tile's prefetch.  Reads are issued together
+// with their lgkmcnt wait in ONE asm statement (early-clobber outputs): an asm output counts as written at the end
+// of its statement, and hipcc does copy such registers right behind the statement (measured: a copy of a
+// ds_read result before a separate wait read stale data).  The data read were retired by earlier counted waits
+// + barriers.
+__device__ __forceinline__ unsigned lds_addr(const void* p) { return (unsigned)(uintptr_t)(PDM_LDS const void*)p; }
+// 8 x 16 B at base + {0, 64, 512, 576, 1024, 1088, 1536, 1600} (a lane's bias / LN-colsum fragments)
+__device__ __forceinline__ void lds_rd_cols(const void* p, f32x4 (&b)[2][2], f32x4 (&c)[2][2]) {
+  asm volatile(
+      "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:64\n\tds_read_b128 %2, %8 offset:512\n\t"
+      "ds_read_b128 %3, %8 offset:576\n\tds_read_b128 %4, %8 offset:1024\n\tds_read_b128 %5, %8 offset:1088\n\t"
+      "ds_read_b128 %6, %8 offset:1536\n\tds_read_b128 %7, %8 offset:1600\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(b[0][0]), "=&v"(b[0][1]), "=&v"(b[1][0]), "=&v"(b[1][1]), "=&v"(c[0][0]), "=&v"(c[0][1]), "=&v"(c[1][0]),
+        "=&v"(c[1][1])
+      : "v"(lds_addr(p))
+      : "memory");
+}
+// 8 x 8 B at base + 8 * {0..7} (a row's raw LN partials)
+__device__ __forceinline__ void lds_rd_raw(const void* p, f32x2 (&v)[8]) {
+  asm volatile(
+      "ds_read_b64 %0, %8\n\tds_read_b64 %1, %8 offset:8\n\tds_read_b64 %2, %8 offset:16\n\t"
+      "ds_read_b64 %3, %8 offset:24\n\tds_read_b64 %4, %8 offset:32\n\tds_read_b64 %5, %8 offset:40\n\t"
+      "ds_read_b64 %6, %8 offset:48\n\tds_read_b64 %7, %8 offset:56\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(lds_addr(p))
+      : "memory");
+}
+// 8 x 8 B at base + {0, 128, 256, 384, 1024, 1152, 1280, 1408} (the (mean, rstd) of a lane's 8 rows)
+__device__ __forceinline__ void lds_rd_rows(const void* p, f32x2 (&v)[8]) {
+  asm volatile(
+      "ds_read_b64 %0, %8\n\tds_read_b64 %1, %8 offset:128\n\tds_read_b64 %2, %8 offset:256\n\t"
+      "ds_read_b64 %3, %8 offset:384\n\tds_read_b64 %4, %8 offset:1024\n\tds_read_b64 %5, %8 offset:1152\n\t"
+      "ds_read_b64 %6, %8 offset:1280\n\tds_read_b64 %7, %8 offset:1408\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(lds_addr(p))
+      : "memory");
+}
+// 4 x 4 B at base + {0, 8, 16, 24} (one row's per-wave sums of one component)
+__device__ __forceinline__ void lds_rd_stat(const void* p, float (&v)[4]) {
+  asm volatile(
+      "ds_read_b32 %0, %4\n\tds_read_b32 %1, %4 offset:8\n\tds_read_b32 %2, %4 offset:16\n\t"
+      "ds_read_b32 %3, %4 offset:24\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+      : "v"(lds_addr(p))
+      : "memory");
+}
+__device__ __forceinline__ void lds_wr64(void* p, float2 v) {
+  const f32x2 w = f32x2{v.x, v.y};
+  asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(p)), "v"(w) : "memory");
+}
+__device__ __forceinline__ void lds_wr32(void* p, float v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// lanes of rows {0,1} and {2,3} exchange: returns (a', b') with a' = [a.r0, b.r0, a.r2, b.r2], b' = [a.r1, b.r1,
+// a.r3, b.r3] (16-lane rows r0..r3); its own inverse
+__device__ __forceinline__ void pl16swap(unsigned& a, unsigned& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n, int ntiles) {
+  static_assert(EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_RES, "persistent kernel epilogues");
+  constexpr int ROWB = 128;
+  constexpr int HALF = 128 * ROWB;
+  constexpr int BUF = 4 * HALF;
+  enum { KA0 = 0, KA1 = 1, KW0 = 2, KW1 = 3 };
+  // VMEM ops every lane issues in an epilogue after its last wait: 16 output stores (+ 1 LN-partial store)
+  constexpr int E = EPI == EPI_RES ? 17 : 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int g4 = lane >> 4, r16 = lane & 15;
+
+  // this workgroup's tiles: the XCD label x = blockIdx % 8 owns a contiguous range of the tile order (gemm8d's
+  // bijective remap), walked by its nx workgroups round robin
+  const int G = gridDim.x, x = blockIdx.x & 7, jw = blockIdx.x >> 3;
+  const int q8 = ntiles >> 3, r8 = ntiles & 7;
+  const int tstart = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+  const int tcnt = q8 + (x < r8 ? 1 : 0);
+  const int nx = (G >> 3) + (x < (G & 7) ? 1 : 0);
+  const int ntl = tcnt > jw ? (tcnt - jw + nx - 1) / nx : 0;
+  if (ntl == 0) return;
+  const int tiles_m = (p.M + BM2 - 1) / BM2;
+  auto tile_mn = [&](int i, int& m0_, int& n0_) {
+    const int u = tstart + jw + i * nx;
+    int tm, tn;
+    if (p.raster > 0) {
+      const int grp = u / (p.raster * tiles_n);
+      const int rows_in = min(p.raster, tiles_m - grp * p.raster);
+      const int r = u - grp * p.raster * tiles_n;
+      tm = grp * p.raster + r % rows_in;
+      tn = r / rows_in;
+    } else {
+      tm = u / tiles_n;
+      tn = u - tm * tiles_n;
+    }
+    m0_ = tm * BM2;
+    n0_ = tn * BN2;
+  };
+
+  // operand descriptors of one tile, based at its first row / column: rows past M (N) lie past num_records and
+  // come back as zeros, so the per-lane offsets below are the same for every tile
+  const int ldw = p.ldw > 0 ? p.ldw : p.K;
+  const bf16* A2 = p.A2 ? p.A2 : p.A1;
+  __amdgpu_buffer_rsrc_t ra1, ra2, rw;
+  auto set_tile = [&](int m0_, int n0_) {
+    ra1 = make_rsrc(p.A1 + (size_t)m0_ * p.lda1, (long long)(p.M - m0_) * p.lda1 * 2);
+    ra2 = make_rsrc(A2 + (size_t)m0_ * p.lda1, (long long)(p.M - m0_) * p.lda1 * 2);
+    rw = make_rsrc(p.W + (size_t)n0_ * ldw, (long long)(p.N - n0_ - 1) * ldw * 2 + (long long)p.K * 2);
+  };
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(p.out_bf16, (long long)p.M * p.ldo * 2);
+  const __amdgpu_buffer_rsrc_t rres = make_rsrc(EPI == EPI_RES && p.accumulate ? p.res_in : p.out_bf16,
+                                                EPI == EPI_RES && p.accumulate ? (long long)p.M * p.ldri * 2 : 0);
+  const bool ln = epi_rowout(EPI) && p.ln_stats != nullptr;
+  const bool stats = EPI == EPI_RES && p.stats_out != nullptr;
+  const __amdgpu_buffer_rsrc_t rst =
+      make_rsrc(stats ? (const void*)p.stats_out : (const void*)p.W, stats ? (long long)p.M * p.stats_ld * 8 : 0);
+
+  // per-lane offsets (tile relative) of this wave's two 1 KiB pieces (8 rows x 128 B) in each half (h) of A and W
+  const int prow = lane >> 3, pch = lane & 7;
+  unsigned aoff[2][2], woff[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + prow;
+    const unsigned sb = (unsigned)((pch ^ ((row >> 1) & 7)) * 16);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      aoff[h][i] = (unsigned)(h * 128 + row) * (unsigned)(p.lda1 * 2) + sb;
+      woff[h][i] = (unsigned)(h * 128 + row) * (unsigned)(ldw * 2) + sb;
+    }
+  }
+  auto issue = [&](int slot, int kt, int kind) {
+    const int k0 = kt * 64;
+    char* dst = smem + slot * BUF + kind * HALF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      PDM_LDS void* d = (PDM_LDS void*)(dst + (wave * 2 + i) * 1024);
+      if (kind >= KW0) dma16(rw, woff[kind - KW0][i], k0 * 2, d);
+      else if (k0 < p.K1) dma16(ra1, aoff[kind][i], k0 * 2, d);
+      else dma16(ra2, aoff[kind][i], (k0 - p.K1) * 2, d);
+    }
+  };
+  // a tile's small tables -> LDS by buffer LDS-DMA (zeros past M / N; hipcc orders LDS reads behind these without
+  // draining vmcnt, unlike the global-address form): the raw LN partials of its 256 rows (contiguous in
+  // ln_stats), bias, LN column sums
+  auto issue_tables = [&](int m0_, int n0_) {
+    if (ln) {
+      const int pieces = p.ln_ld * 2;   // KiB
+      const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.ln_stats + (size_t)m0_ * p.ln_ld * 2, (long long)(p.M - m0_) * p.ln_ld * 8);
+      for (int pc = wave; pc < pieces; pc += 8)
+        dma16(rr, (unsigned)(pc * 1024 + lane * 16), 0, (PDM_LDS void*)(smem + S_RAW + pc * 1024));
+      if (wave == 7)
+        dma16(make_rsrc(p.ln_colsum + n0_, (long long)(p.N - n0_) * 4), (unsigned)(lane * 16), 0,
+              (PDM_LDS void*)(smem + S_COL + 1024));
+    }
+    if (wave == 6 && p.bias)
+      dma16(make_rsrc(p.bias + n0_, (long long)(p.N - n0_) * 4), (unsigned)(lane * 16), 0, (PDM_LDS void*)(smem + S_COL));
+  };
+
+  bf16x8 af[4][2];
+  bf16x8 wf[2][2][2];
+  auto read_a = [&](const char* buf, int qi) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int row = wm * 64 + mi * 16 + r16;
+        af[mi][ks] = *reinterpret_cast<const bf16x8*>(buf + qi * HALF + swz_off<64>(row, ks * 4 + g4));
+      }
+  };
+  auto read_w = [&](const char* buf, int qj) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int row = wn * 32 + ni * 16 + r16;
+        wf[qj][ni][ks] = *reinterpret_cast<const bf16x8*>(buf + (2 + qj) * HALF + swz_off<64>(row, ks * 4 + g4));
+      }
+  };
+  auto lds_done = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  f32x4 acc[32];
+  auto mma = [&](int qi, int qj) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          f32x4& c = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
+          c = mfma16x16x32(wf[qj][ni][ks], af[mi][ks], c);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = p.K / 64;   // >= 4 (gemm_launch)
+  int m0, n0;
+  tile_mn(0, m0, n0);
+  set_tile(m0, n0);
+  // prologue of the first tile: tables, K-tile 0, A0 W0 W1 of K-tile 1; the wait retires the tables and A0 W0 W1(0)
+  issue_tables(m0, n0);
+  issue(0, 0, KA0);
+  issue(0, 0, KW0);
+  issue(0, 0, KW1);
+  issue(0, 0, KA1);
+  issue(1, 1, KA0);
+  issue(1, 1, KW0);
+  issue(1, 1, KW1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  bar_raw();
+
+  for (int it = 0; it < ntl; ++it) {
+    const bool has_next = it + 1 < ntl;
+    int m0n = 0, n0n = 0;
+    if (has_next) tile_mn(it + 1, m0n, n0n);
+#pragma unroll
+    for (int f = 0; f < 32; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int par = (it * nk) & 1;   // ring slot of the tile's K-tile 0
+    if (wave >= 4) bar_raw();        // stagger: waves 4-7 one barrier behind
+    for (int kt = 0; kt < nk; ++kt) {
+      const int slot = (par + kt) & 1;
+      const char* buf = smem + slot * BUF;
+      // the previous tile's epilogue stores (E per lane) are younger than the ring loads this K-tile waits for
+      const bool after_epi = kt == 0 && it > 0;
+      const bool m1 = kt + 1 < nk || has_next;   // K-tile g+1 exists (this tile's kt+1 or the next tile's 0)
+      const bool m2 = kt + 2 < nk || has_next;   // K-tile g+2 (nk >= 4: the next tile's kt+2-nk <= 1)
+      // phase A: quadrants (0,0) (0,1); issues A1 of K-tile g+1
+      read_a(buf, 0);
+      read_w(buf, 0);
+      read_w(buf, 1);
+      lds_done();
+      if (m1) {
+        issue(slot ^ 1, kt + 1 < nk ? kt + 1 : 0, KA1);
+        if (after_epi) wait_vmcnt_n<8 + E>();
+        else wait_vmcnt_n<8>();
+      } else {
+        wait_vmcnt_n<0>();
+      }
+      bar_raw();
+      mma(0, 0);
+      mma(0, 1);
+      bar_raw();
+      // phase B: quadrants (1,0) (1,1); issues A0 W0 W1 of K-tile g+2 (the next tile's from kt = nk-2 on)
+      read_a(buf, 1);
+      lds_done();
+      if (kt == nk - 2 && has_next) set_tile(m0n, n0n);
+      if (m2) {
+        const int k2 = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
+        issue(slot, k2, KA0);
+        issue(slot, k2, KW0);
+        issue(slot, k2, KW1);
+        if (after_epi) wait_vmcnt_n<8 + E>();
+        else wait_vmcnt_n<8>();
+      } else if (m1) {
+        wait_vmcnt_n<2>();
+      }
+      bar_raw();
+      mma(1, 0);
+      mma(1, 1);
+      bar_raw();
+    }
+    if (wave < 4) bar_raw();   // rejoin the stagger
+
+    if (p.dbg_tile0 & 16) {    // timing experiment: no epilogue (its E stores still issued, to nowhere)
+#pragma unroll
+      for (int f = 0; f < 32; ++f) asm volatile("" ::"v"(acc[f]));
+      if (has_next) issue_tables(m0n, n0n);
+#pragma unroll
+      for (int s = 0; s < E; ++s) __builtin_amdgcn_raw_buffer_store_b32(0, rout, (int)OOB, 0, 0);
+      m0 = m0n;
+      n0 = n0n;
+      continue;
+    }
+
+    // ---- epilogue of tile (m0, n0) ----
+    // this lane's columns: fragment (qj, ni) covers n0 + qj*128 + wn*32 + ni*16 + g4*4 + [0, 4)
+    f32x4 bv[2][2], cs[2][2];
+    lds_rd_cols(smem + S_COL + (wn * 32 + g4 * 4) * 4, bv, cs);
+    char* lnrow = smem + S_LNROW;
+    if (ln && tid < 256) {
+      f32x2 raw[8];
+      lds_rd_raw(smem + S_RAW + tid * p.ln_ld * 8, raw);
+      float2 lst[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) lst[t] = t < p.ln_ld ? make_float2(raw[t][0], raw[t][1]) : make_float2(0.f, 0.f);
+      lds_wr64(lnrow + tid * 8, ln_from_partials(lst, p.ln_ld, p.ln_D, p.ln_eps, nullptr));
+    }
+    lds_sync();
+#pragma unroll
+    for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        if (!p.bias) bv[qj][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!ln) cs[qj][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    bar_raw();   // lnrow complete; the raw / column tables are free for the next tile's
+    if (has_next) issue_tables(m0n, n0n);
+    const int offg = (g4 & 1) * 16 + (g4 >> 1) * 8;   // post-swap column offset of the lane's 8 columns
+    float2 mrow[2][4];   // (mean, rstd) of the lane's 8 rows
+    {
+      f32x2 mr8[8];
+      lds_rd_rows(lnrow + (wm * 64 + r16) * 8, mr8);
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+          mrow[qi][mi] = ln ? make_float2(mr8[qi * 4 + mi][0], mr8[qi * 4 + mi][1]) : make_float2(0.f, 1.f);
+    }
+
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const int ml = qi * 128 + wm * 64 + mi * 16 + r16;
+          const float2 mr = mrow[qi][mi];
+          const int m = m0 + ml;
+#pragma unroll
+          for (int qj = 0; qj < 2; ++qj) {
+            unsigned u[2][2];
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+              f32x4 v = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
+              if (ln) v = (v - mr.x * cs[qj][ni]) * mr.y;
+              v += bv[qj][ni];
+              if constexpr (EPI == EPI_GELU) {   // exact-erf GELU only (quick GELU: gemm8d, fits_8s)
+                const f32x2 lo = gelu_erf2(f32x2{v[0], v[1]}), hi = gelu_erf2(f32x2{v[2], v[3]});
+                v = f32x4{lo[0], lo[1], hi[0], hi[1]};
+              }
+              u[ni][0] = pack_bf16x2(v[0], v[1]);
+              u[ni][1] = pack_bf16x2(v[2], v[3]);
+            }
+            pl16swap(u[0][0], u[1][0]);
+            pl16swap(u[0][1], u[1][1]);
+            const int n = n0 + qj * 128 + wn * 32 + offg;
+            const unsigned off = (m < p.M && n < p.N) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)u[0][0], (int)u[0][1], (int)u[1][0], (int)u[1][1]},
+                                                   rout, (int)off, 0, 0);
+          }
+        }
+    } else {   // EPI_RES
+      // residual rows in the 16-byte layout (zeros out of range), all issued before the first use
+      i32x4 rr[2][4][2];
+      const bool acc_res = p.accumulate != 0;
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int qj = 0; qj < 2; ++qj) {
+            const int m = m0 + qi * 128 + wm * 64 + mi * 16 + r16, n = n0 + qj * 128 + wn * 32 + offg;
+            const unsigned off =
+                (acc_res && m < p.M && n < p.N) ? ((unsigned)m * (unsigned)p.ldri + (unsigned)n) * 2u : OOB;
+            rr[qi][mi][qj] = __builtin_amdgcn_raw_buffer_load_b128(rres, (int)off, 0, 0);
+          }
+      const int ncols = min(256, p.N - n0);
+      float rsum[2][4];
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const int ml = qi * 128 + wm * 64 + mi * 16 + r16;
+          const int m = m0 + ml;
+          float s = 0.f;
+#pragma unroll
+          for (int qj = 0; qj < 2; ++qj) {
+            unsigned r0 = (unsigned)rr[qi][mi][qj][0], r1 = (unsigned)rr[qi][mi][qj][1];
+            unsigned r2 = (unsigned)rr[qi][mi][qj][2], r3 = (unsigned)rr[qi][mi][qj][3];
+            pl16swap(r0, r2);   // back to the fragment layout: (r0, r1) = fragment ni 0, (r2, r3) = ni 1
+            pl16swap(r1, r3);
+            const unsigned rs[2][2] = {{r0, r1}, {r2, r3}};
+            unsigned u[2][2];
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+              f32x4& v = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
+              v += bv[qj][ni];
+              v[0] += bf16lo(rs[ni][0]); v[1] += bf16hi(rs[ni][0]);
+              v[2] += bf16lo(rs[ni][1]); v[3] += bf16hi(rs[ni][1]);
+              u[ni][0] = pack_bf16x2(v[0], v[1]);
+              u[ni][1] = pack_bf16x2(v[2], v[3]);
+              // the rounded values feed the partials (exactly what the next GEMM reads); columns past N are 0
+              const bool valid = qj * 128 + wn * 32 + ni * 16 + g4 * 4 < ncols;
+              v = valid ? f32x4{bf16lo(u[ni][0]), bf16hi(u[ni][0]), bf16lo(u[ni][1]), bf16hi(u[ni][1])}
+                        : f32x4{0.f, 0.f, 0.f, 0.f};
+              s += (v[0] + v[1]) + (v[2] + v[3]);
+            }
+            pl16swap(u[0][0], u[1][0]);
+            pl16swap(u[0][1], u[1][1]);
+            const int n = n0 + qj * 128 + wn * 32 + offg;
+            const unsigned off = (m < p.M && n < p.N) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)u[0][0], (int)u[0][1], (int)u[1][0], (int)u[1][1]},
+                                                   rout, (int)off, 0, 0);
+          }
+          rsum[qi][mi] = s;
+        }
+      // LayerNorm partials of the 256-column group: row sums over the wave's 4 lane rows, then over the 4 column
+      // waves (wn) through LDS; M2 about the group mean the same way.  Without stats_out the store still issues
+      // (to nowhere), so every epilogue has E VMEM ops.
+      char* tab = smem + S_STAT;   // [row][wn][sum, m2] fp32
+      if (stats) {
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) {
+            const float s = xrow_sum4(rsum[qi][mi]);
+            if (g4 == 0) lds_wr32(tab + ((qi * 128 + wm * 64 + mi * 16 + r16) * 4 + wn) * 8, s);
+          }
+      }
+      lds_sync();
+      bar_raw();
+      if (stats) {
+        const float inv = 1.0f / (float)ncols;
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) {
+            const int ml = qi * 128 + wm * 64 + mi * 16 + r16;
+            float t4[4];
+            lds_rd_stat(tab + ml * 32, t4);
+            const float mu = ((t4[0] + t4[1]) + (t4[2] + t4[3])) * inv;
+            float q = 0.f;
+#pragma unroll
+            for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+              for (int ni = 0; ni < 2; ++ni) {
+                const f32x4 d = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi] - mu;
+                const bool valid = qj * 128 + wn * 32 + ni * 16 + g4 * 4 < ncols;
+                const float dq = (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+                q += valid ? dq : 0.f;
+              }
+            q = xrow_sum4(q);
+            if (g4 == 0) lds_wr32(tab + (ml * 4 + wn) * 8 + 4, q);
+          }
+      }
+      lds_sync();
+      bar_raw();
+      {   // one float per thread: row tid >> 1, component tid & 1 (sum, M2)
+        const int ml = tid >> 1, c = tid & 1;
+        float t4[4];
+        lds_rd_stat(tab + ml * 32 + c * 4, t4);
+        const float v = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+        const int m = m0 + ml;
+        const unsigned off = (stats && m < p.M) ? (unsigned)((m * p.stats_ld + (n0 >> 8)) * 2 + c) * 4u : OOB;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), rst, (int)off, 0, 0);
+      }
+    }
+    m0 = m0n;
+    n0 = n0n;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Tall tile for N <= 128 (algo 9; the decoder's 128-channel 512^2 convs): 512 x 128 per workgroup, 8 waves.
 // A 256 x 128 tile re-fetches its 32 KiB A K-tile for half the MFMA work of a 256 x 256 one and runs at the
 // same time per K-tile (tools/conv_bench.py: algo 8 ~ algo 1 ~ 0.58 PF on these convs), so the N = 128 GEMM
@@ -1884,6 +2401,48 @@ static hipError_t launch8d(const GemmArgs& p, int epi, hipStream_t stream) {
   return hipGetLastError();
 }
 
+static int g_num_cus = 0;
+static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_GELU>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_RES>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_num_cus = n;
+    else
+      g_num_cus = 256;
+    attr_set = true;
+  }
+  const int tn = (p.N + BN2 - 1) / BN2, tm = (p.M + BM2 - 1) / BM2;
+  const int ntiles = tm * tn;
+  const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL(gemm8s_kernel<EPI_BF16>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
+    case EPI_GELU: hipLaunchKernelGGL(gemm8s_kernel<EPI_GELU>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
+    case EPI_RES: hipLaunchKernelGGL(gemm8s_kernel<EPI_RES>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// the persistent kernel's preconditions (epilogues, no conv / batch / gather / MXFP8, K >= 256, one A stride,
+// buffer extents)
+static bool fits_8s(const GemmArgs& p, int epi) {
+  const long long lim = 0x7fffffffLL;
+  if (epi != EPI_BF16 && epi != EPI_GELU && epi != EPI_RES) return false;
+  if (p.conv || p.batch > 1 || p.a_rows_per_group > 0 || p.out_fp8 || p.fp8 || p.mx_center || !p.out_bf16) return false;
+  if (epi == EPI_GELU && p.act) return false;
+  if (p.K < 256 || (p.A2 && p.K1 < p.K && p.lda2 != p.lda1) || p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15) || (p.ln_stats && p.ln_ld > 8)) return false;
+  if ((long long)p.M * p.ldo * 2 >= lim) return false;
+  if (epi == EPI_RES && p.accumulate && (p.ldri % 8 || ((uintptr_t)p.res_in & 15) || (long long)p.M * p.ldri * 2 >= lim))
+    return false;
+  if (p.stats_out && (long long)p.M * p.stats_ld * 8 >= lim) return false;
+  if (p.dbg_tile0 & 15) return false;   // gemm8d's timing modes
+  return fits_rsrc(p);
+}
+
 static hipError_t launch_mx(const GemmArgs& p, int epi, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
@@ -1931,8 +2490,14 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
   // 96 < N <= 128 with many rows (the decoder's 128-channel 512^2 convs and nin_shortcut): the 512 x 128 tall
   // tile, algo 9 (conv 128 -> 128 at 512^2 x 8 images: 870 us vs 1059 us on the 128 tile; the 256 x 128 half-N
   // tile, algo 8, measured 1070 us and is kept as an option only: tools/conv_bench.py, profiles/r03q)
-  if (algo == 0)
+  if (algo == 0) {
     algo = (rows_all >= 4096 && p.N >= 256) ? 7 : (rows_all >= 65536 && p.N > 96 && p.N <= 128 && p.batch <= 1) ? 9 : 1;
+    if (algo == 7 && fits_8s(p, epi)) algo = 11;   // the persistent kernel where its epilogues apply
+  }
+  if (algo == 11) {
+    if (!p.fp8 && fits_8s(p, epi)) return launch8s(p, epi, stream);
+    algo = 7;
+  }
   if ((algo == 8 || algo == 9) && (p.N > 128 || (epi != EPI_BF16 && epi != EPI_F32) || p.ln_stats || p.stats_out ||
                                     p.out_fp8 || p.a_rows_per_group > 0 || (algo == 9 && p.batch > 1))) algo = 1;
   // the 256-tile bf16 epilogue stores 16-byte row chunks: needs N, ldo multiples of 8 and an aligned output

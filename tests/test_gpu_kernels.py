@@ -47,13 +47,13 @@ def test_gemm(lib, M, N, K, epi):
         assert rel(out, ref + r0) < 2e-3
 
 
-@pytest.mark.parametrize("algo", [0, 1, 7])
+@pytest.mark.parametrize("algo", [0, 1, 7, 11])
 def test_gelu_activation_exactness(lib, algo):
     """The GELU epilogue alone: A's column 0 carries x, W = e_0, so C = x exactly in fp32 and the output is the
     bf16 rounding of the kernel's GELU(x).  Against exact-erf GELU in fp64: within one bf16 ulp everywhere
     or 2e-5 absolute where GELU ~ 0 (the polynomial's own error is <= 1.8e-5 abs / 9.5e-4 rel,
     csrc/pdm_common.h), exact 0 / x in the tails."""
-    M, N, K = 4096, 256, 64
+    M, N, K = 4096, 256, 256   # K >= 256: the persistent kernel (algo 11) applies too
     xs = torch.linspace(-8.0, 8.0, M, device="cuda").bfloat16()
     a = torch.zeros(M, K, device="cuda", dtype=torch.bfloat16)
     a[:, 0] = xs
@@ -85,7 +85,7 @@ def test_gemm_split_k(lib):
     assert rel(out, ref) < 2e-3
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7, 8, 9, 11])
 @pytest.mark.parametrize("M,N,K", [(4133, 1000, 1024), (515, 768, 2048), (8192, 512, 128), (700, 264, 64),
                                    (1100, 520, 192), (5000, 128, 1152), (700, 120, 64)])
 @pytest.mark.parametrize("epi", ["gelu", "f32acc_copy", "split"])
@@ -213,7 +213,7 @@ def test_rowstats(lib, rows, D):
     assert rel(st, ref) < 1e-5
 
 
-@pytest.mark.parametrize("algo", [1, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("algo", [1, 3, 4, 5, 6, 7, 11])
 @pytest.mark.parametrize("M,N,K,epi", [(4133, 1024, 1024, "bf16"), (515, 4096, 1024, "gelu"), (9000, 3456, 1152, "bf16"),
                                        (700, 520, 512, "gelu")])
 def test_gemm_layernorm_consumer(lib, algo, M, N, K, epi):
@@ -261,7 +261,7 @@ def test_gemm_layernorm_producer(lib, algo, M, N, K):
     assert rel(st, _ref_partials(out)) < 1e-5
 
 
-@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("algo", [0, 1, 7, 11])
 @pytest.mark.parametrize("M,N,K,mode", [(4133, 1024, 1024, "inplace"), (515, 1152, 2048, "outofplace"),
                                         (8192, 512, 256, "noacc"), (300, 264, 64, "inplace")])
 def test_gemm_residual_bf16(lib, algo, M, N, K, mode):
@@ -308,6 +308,54 @@ def test_gemm_residual_f32_out_of_place(lib, algo, M, N, K):
     assert torch.equal(res, res0)
     assert rel(out, ref) < 2e-3
     assert torch.equal(cp, out.bfloat16())
+
+
+@pytest.mark.parametrize("M,N,K,kind", [(25800, 3072, 1024, "ln"), (25800, 4096, 1024, "ln_gelu"),
+                                        (12937, 1024, 1024, "res"), (25800, 1024, 4096, "res"), (12900, 1024, 2048, "skip"),
+                                        (9137, 1152, 1152, "res"), (9137, 3456, 1152, "ln"), (6000, 4608, 1152, "ln_gelu"),
+                                        (70000, 512, 256, "res"), (5000, 1152, 256, "bf16"), (300, 264, 512, "res")])
+def test_gemm_persistent(lib, M, N, K, kind):
+    """The persistent 256-tile kernel (algo 11, several tiles per workgroup, the LDS-DMA ring running across tile
+    boundaries, permlane-swapped 16-byte stores, in-register residual epilogue) against the per-tile kernel (algo 7):
+    the same MFMA chain, so the outputs are bit-identical (the LayerNorm-consumer epilogue within one bf16 rounding:
+    the compiler contracts its fused terms differently); its LayerNorm partials (a different summation order)
+    against float64 torch.  Ragged M, N % 256 != 0 (the 128-wide last column tile), split-K, D = 1152 (5 partials
+    per row), K = 256 (4 K-tiles: the shortest the kernel takes)."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + 3)
+    Ka = K // 2 if kind == "skip" else K
+    a = torch.randn(M, Ka, device="cuda", generator=g).bfloat16()
+    a2 = torch.randn(M, K - Ka, device="cuda", generator=g).bfloat16() if kind == "skip" else None
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    outs = {}
+    for algo in (7, 11):
+        lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
+        try:
+            if kind in ("ln", "ln_gelu"):
+                x = torch.randn(M, K, device="cuda", generator=torch.Generator(device="cuda").manual_seed(9)) * 1.5 + 2.0
+                xb, st = lib.rowstats(x)
+                colsum = w.double().sum(1).float()
+                outs[algo] = (lib.gemm_ln(xb, w, bias, lib.EPI_GELU if kind == "ln_gelu" else lib.EPI_BF16, ln_stats=st,
+                                          ln_colsum=colsum),)
+            elif kind == "bf16":
+                outs[algo] = (lib.gemm(a, w, bias, lib.EPI_BF16),)
+            else:
+                res = (torch.randn(M, N, device="cuda", generator=torch.Generator(device="cuda").manual_seed(4)) * 3 +
+                       2.0).bfloat16()
+                out = res.clone()
+                st = torch.full((M, (N + 255) // 256, 2), float("nan"), device="cuda")
+                lib.gemm_ex(lib.EPI_RES, a, w, bias, out=out, res_in=out, accumulate=True, stats_out=st, a2=a2)
+                outs[algo] = (out, st)
+        finally:
+            lib.load().pdm_set_gemm_algo(0)
+    if kind in ("ln", "ln_gelu"):
+        d = (outs[7][0].float() - outs[11][0].float()).abs()
+        assert rel(outs[11][0].float(), outs[7][0].float()) < 1e-3 and float((d > 0).float().mean()) < 1e-3
+    else:
+        assert torch.equal(outs[7][0], outs[11][0])
+    if kind in ("res", "skip"):
+        assert rel(outs[11][1], _ref_partials(outs[11][0].float())) < 1e-5
+        assert rel(outs[7][1], outs[11][1]) < 1e-5
 
 
 def test_gemm_bad_shape(lib):

@@ -1,8 +1,8 @@
 """Speed-of-light decomposition of one eager U-ViT forward (dev tool): the same forward timed with parts of the
 GEMM family switched off by pdm_set_gemm_tuning timing bits (wrong results, timing only), interleaved in one
 process so the variants share the box's clock state.
-  normal      the forward as shipped
-  noepi       bit 16: every 256-tile GEMM skips its epilogue (main loops only; nothing written)
+  a11 / a7    the forward with the persistent GEMM (algo 11, the default) / the per-tile GEMM (algo 7)
+  noepi11/7   timing bit 16: every 256-tile GEMM skips its epilogue (main loops only; nothing written)
 usage: python tools/sol_forward.py [config] [rows] [rounds]"""
 import sys
 import time
@@ -30,14 +30,15 @@ if cfg["name"] == "uvit_t2i":
              torch.randn(rows, cfg["num_panoptic_class"], *zs[1:], device=dev))
 else:
     extra = (torch.randint(0, 1000, (rows,), device=dev) if cfg.get("num_classes", -1) > 0 else None,)
-modes = {"normal": 0, "noepi": 16}
+modes = {"a11": (11, 0), "a7": (7, 0), "noepi11": (11, 16), "noepi7": (7, 16)}
 res = {k: [] for k in modes}
 with torch.no_grad():
     for _ in range(20):
         net.forward_pre(x, t, *extra)
     torch.cuda.synchronize()
     for r in range(rounds):
-        for k, dbg in modes.items():
+        for k, (algo, dbg) in modes.items():
+            lib.pdm_set_gemm_algo(algo)
             lib.pdm_set_gemm_tuning(0, dbg)
             net.forward_pre(x, t, *extra)
             torch.cuda.synchronize()
@@ -47,6 +48,7 @@ with torch.no_grad():
             torch.cuda.synchronize()
             res[k].append((time.perf_counter() - t0) / 5 * 1e3)
     lib.pdm_set_gemm_tuning(0, 0)
+    lib.pdm_set_gemm_algo(0)
 for k, v in res.items():
     v = sorted(v)
     print(f"{name} rows={rows} {k:8s} median {v[len(v) // 2]:.2f} ms/forward  min {v[0]:.2f}", flush=True)
