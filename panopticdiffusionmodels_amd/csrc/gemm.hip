@@ -1303,11 +1303,11 @@ __device__ __forceinline__ void lds_rd_rows(const void* p, f32x2 (&v)[8]) {
       : "v"(lds_addr(p))
       : "memory");
 }
-// 4 x 4 B at base + {0, 8, 16, 24} (one row's per-wave sums of one component)
-__device__ __forceinline__ void lds_rd_stat(const void* p, float (&v)[4]) {
+// 4 x 8 B at base + {0, 8, 16, 24} (one row's per-wave (sum, M2) pairs)
+__device__ __forceinline__ void lds_rd_stat2(const void* p, f32x2 (&v)[4]) {
   asm volatile(
-      "ds_read_b32 %0, %4\n\tds_read_b32 %1, %4 offset:8\n\tds_read_b32 %2, %4 offset:16\n\t"
-      "ds_read_b32 %3, %4 offset:24\n\ts_waitcnt lgkmcnt(0)"
+      "ds_read_b64 %0, %4\n\tds_read_b64 %1, %4 offset:8\n\tds_read_b64 %2, %4 offset:16\n\t"
+      "ds_read_b64 %3, %4 offset:24\n\ts_waitcnt lgkmcnt(0)"
       : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
       : "v"(lds_addr(p))
       : "memory");
@@ -1315,9 +1315,6 @@ __device__ __forceinline__ void lds_rd_stat(const void* p, float (&v)[4]) {
 __device__ __forceinline__ void lds_wr64(void* p, float2 v) {
   const f32x2 w = f32x2{v.x, v.y};
   asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(p)), "v"(w) : "memory");
-}
-__device__ __forceinline__ void lds_wr32(void* p, float v) {
-  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
 }
 __device__ __forceinline__ void lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1600,8 +1597,9 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni) {
               f32x4 v = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
-              if (ln) v = (v - mr.x * cs[qj][ni]) * mr.y;
-              v += bv[qj][ni];
+              // rstd * (acc - mean * colsum) + bias as acc * rstd + (bias - mean * rstd * colsum): 2 FMAs per value
+              if (ln) v = v * mr.y + (bv[qj][ni] - (mr.x * mr.y) * cs[qj][ni]);
+              else v += bv[qj][ni];
               if constexpr (EPI == EPI_GELU) {   // exact-erf GELU only (quick GELU: gemm8d, fits_8s)
                 const f32x2 lo = gelu_erf2(f32x2{v[0], v[1]}), hi = gelu_erf2(f32x2{v[2], v[3]});
                 v = f32x4{lo[0], lo[1], hi[0], hi[1]};
@@ -1612,7 +1610,7 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
             pl16swap(u[0][0], u[1][0]);
             pl16swap(u[0][1], u[1][1]);
             const int n = n0 + qj * 128 + wn * 32 + offg;
-            const unsigned off = (m < p.M && n < p.N) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
+            const unsigned off = (m < p.M && n < p.N && !(p.dbg_tile0 & 32)) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
             __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)u[0][0], (int)u[0][1], (int)u[1][0], (int)u[1][1]},
                                                    rout, (int)off, 0, 0);
           }
@@ -1628,8 +1626,8 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
 #pragma unroll
           for (int qj = 0; qj < 2; ++qj) {
             const int m = m0 + qi * 128 + wm * 64 + mi * 16 + r16, n = n0 + qj * 128 + wn * 32 + offg;
-            const unsigned off =
-                (acc_res && m < p.M && n < p.N) ? ((unsigned)m * (unsigned)p.ldri + (unsigned)n) * 2u : OOB;
+            const unsigned off = (acc_res && m < p.M && n < p.N && !(p.dbg_tile0 & 64))
+                                     ? ((unsigned)m * (unsigned)p.ldri + (unsigned)n) * 2u : OOB;
             rr[qi][mi][qj] = __builtin_amdgcn_raw_buffer_load_b128(rres, (int)off, 0, 0);
           }
       const int ncols = min(256, p.N - n0);
@@ -1666,37 +1664,27 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
             pl16swap(u[0][0], u[1][0]);
             pl16swap(u[0][1], u[1][1]);
             const int n = n0 + qj * 128 + wn * 32 + offg;
-            const unsigned off = (m < p.M && n < p.N) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
+            const unsigned off = (m < p.M && n < p.N && !(p.dbg_tile0 & 32)) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
             __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)u[0][0], (int)u[0][1], (int)u[1][0], (int)u[1][1]},
                                                    rout, (int)off, 0, 0);
           }
           rsum[qi][mi] = s;
         }
-      // LayerNorm partials of the 256-column group: row sums over the wave's 4 lane rows, then over the 4 column
-      // waves (wn) through LDS; M2 about the group mean the same way.  Without stats_out the store still issues
-      // (to nowhere), so every epilogue has E VMEM ops.
+      // LayerNorm partials of the 256-column group (sum, M2 about the group mean): every wave reduces its own 64
+      // columns of a row (sum over the 4 lane rows, M2 about the wave's own mean) and the 4 column waves (wn) are
+      // merged with Chan's update through LDS -- one barrier.  Without stats_out the store still issues (to
+      // nowhere), so every epilogue has E VMEM ops.
       char* tab = smem + S_STAT;   // [row][wn][sum, m2] fp32
+      auto wave_cols = [&](int w) { return max(0, min(32, ncols - w * 32)) + max(0, min(32, ncols - 128 - w * 32)); };
       if (stats) {
+        const int nw = wave_cols(wn);
+        const float inv_w = nw > 0 ? 1.0f / (float)nw : 0.f;
 #pragma unroll
         for (int qi = 0; qi < 2; ++qi)
 #pragma unroll
           for (int mi = 0; mi < 4; ++mi) {
-            const float s = xrow_sum4(rsum[qi][mi]);
-            if (g4 == 0) lds_wr32(tab + ((qi * 128 + wm * 64 + mi * 16 + r16) * 4 + wn) * 8, s);
-          }
-      }
-      lds_sync();
-      bar_raw();
-      if (stats) {
-        const float inv = 1.0f / (float)ncols;
-#pragma unroll
-        for (int qi = 0; qi < 2; ++qi)
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) {
-            const int ml = qi * 128 + wm * 64 + mi * 16 + r16;
-            float t4[4];
-            lds_rd_stat(tab + ml * 32, t4);
-            const float mu = ((t4[0] + t4[1]) + (t4[2] + t4[3])) * inv;
+            const float sw = xrow_sum4(rsum[qi][mi]);
+            const float mu = sw * inv_w;
             float q = 0.f;
 #pragma unroll
             for (int qj = 0; qj < 2; ++qj)
@@ -1708,16 +1696,27 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
                 q += valid ? dq : 0.f;
               }
             q = xrow_sum4(q);
-            if (g4 == 0) lds_wr32(tab + (ml * 4 + wn) * 8 + 4, q);
+            if (g4 == 0) lds_wr64(tab + ((qi * 128 + wm * 64 + mi * 16 + r16) * 4 + wn) * 8, make_float2(sw, q));
           }
       }
       lds_sync();
       bar_raw();
       {   // one float per thread: row tid >> 1, component tid & 1 (sum, M2)
         const int ml = tid >> 1, c = tid & 1;
-        float t4[4];
-        lds_rd_stat(tab + ml * 32 + c * 4, t4);
-        const float v = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+        f32x2 t4[4];
+        lds_rd_stat2(tab + ml * 32, t4);
+        const float S = (t4[0][0] + t4[1][0]) + (t4[2][0] + t4[3][0]);
+        float v = S;
+        if (c) {
+          const float mean = S / (float)ncols;
+          v = 0.f;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const int nw = wave_cols(w);
+            const float d = nw > 0 ? t4[w][0] / (float)nw - mean : 0.f;
+            v += t4[w][1] + (float)nw * d * d;
+          }
+        }
         const int m = m0 + ml;
         const unsigned off = (stats && m < p.M) ? (unsigned)((m * p.stats_ld + (n0 >> 8)) * 2 + c) * 4u : OOB;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), rst, (int)off, 0, 0);

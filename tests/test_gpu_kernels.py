@@ -317,9 +317,9 @@ def test_gemm_residual_f32_out_of_place(lib, algo, M, N, K):
 def test_gemm_persistent(lib, M, N, K, kind):
     """The persistent 256-tile kernel (algo 11, several tiles per workgroup, the LDS-DMA ring running across tile
     boundaries, permlane-swapped 16-byte stores, in-register residual epilogue) against the per-tile kernel (algo 7):
-    the same MFMA chain, so the outputs are bit-identical (the LayerNorm-consumer epilogue within one bf16 rounding:
-    the compiler contracts its fused terms differently); its LayerNorm partials (a different summation order)
-    against float64 torch.  Ragged M, N % 256 != 0 (the 128-wide last column tile), split-K, D = 1152 (5 partials
+    the same MFMA chain, so the outputs are bit-identical (the LayerNorm-consumer epilogue to fp32 rounding: it applies
+    rstd * (acc - mean * colsum) + bias as acc * rstd + (bias - mean * rstd * colsum), so a few bf16 roundings flip);
+    its LayerNorm partials (per-wave partials merged with Chan's update) against float64 torch.  Ragged M, N % 256 != 0 (the 128-wide last column tile), split-K, D = 1152 (5 partials
     per row), K = 256 (4 K-tiles: the shortest the kernel takes)."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K + 3)
     Ka = K // 2 if kind == "skip" else K
@@ -350,7 +350,7 @@ def test_gemm_persistent(lib, M, N, K, kind):
             lib.load().pdm_set_gemm_algo(0)
     if kind in ("ln", "ln_gelu"):
         d = (outs[7][0].float() - outs[11][0].float()).abs()
-        assert rel(outs[11][0].float(), outs[7][0].float()) < 1e-3 and float((d > 0).float().mean()) < 1e-3
+        assert rel(outs[11][0].float(), outs[7][0].float()) < 1e-3 and float((d > 0).float().mean()) < 2e-2
     else:
         assert torch.equal(outs[7][0], outs[11][0])
     if kind in ("res", "skip"):

@@ -79,6 +79,10 @@ for name, N, K, kind in shapes:
             finally:
                 lib.pdm_set_gemm_tuning(0, 0)
         return run
+    if ALGO == 11:   # the persistent kernel's timing bits: 16 no epilogue, 32 stores dropped, 64 residual loads dropped
+        fwd = {"qkv": "ln_bf16", "proj": "res_acc_st", "fc1": "ln_gelu", "fc2": "res_acc_st", "skip": "res_acc_st"}[name]
+        for nm, bit in (("noepi", 16), ("dropst", 32), ("dropres", 64), ("dropboth", 96)):
+            variants[fwd + "_" + nm] = tuned(bit, variants[fwd])
     variants["nostore"] = tuned(2, lambda: _lib.gemm_ex(_lib.EPI_BF16, a, W, bias))
     variants["halfstore"] = tuned(4, lambda: _lib.gemm_ex(_lib.EPI_BF16, a, W, bias, out=o))
     # every row tile stores onto rows 0..255 (an L2-resident 256 x N output): the store cost without HBM write-back
