@@ -399,10 +399,11 @@ def test_attention(lib, L, Dh, q_log2):
 
 
 @pytest.mark.parametrize("algo", [1, 2, 3, 4])
-@pytest.mark.parametrize("L", [17, 66, 257, 258, 334, 590])
+@pytest.mark.parametrize("L", [17, 66, 129, 257, 258, 334, 513, 590])
 def test_attention_algos(lib, algo, L):
     """Both attention structures (1: streamed K/V per 64-query block; 2/3: head-resident K/V, 2 or 3 query
-    tiles per wave) at Dh = 64 on ragged lengths (the head-resident path declines shapes it cannot hold)."""
+    tiles per wave; 4: head-resident v2, a ragged last tile at nqt = k NW + 1 (L = 66, 129, 257, 258, 513) run as the
+    third tile of a pass) at Dh = 64 on ragged lengths (the head-resident path declines shapes it cannot hold)."""
     H, B, Dh = 4, 3, 64
     D = H * Dh
     g = torch.Generator(device="cuda").manual_seed(L + algo)
