@@ -1329,15 +1329,19 @@ __device__ __forceinline__ void pl16swap(unsigned& a, unsigned& b) {
   b = r[1];
 }
 
-template <int EPI>
+// MXO = 1 (bf16 / GELU only): the output is the MXFP8 copy alone (out_fp8 + out_scale, no bf16 rows): the H/4 bf16
+// fc1 whose GELU epilogue emits the fp8 fc2 operand (capi.hip run_block8)
+template <int EPI, int MXO = 0>
 __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n, int ntiles) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_RES, "persistent kernel epilogues");
+  static_assert(!MXO || EPI != EPI_RES, "MXFP8 output: bf16 / GELU epilogues");
   constexpr int ROWB = 128;
   constexpr int HALF = 128 * ROWB;
   constexpr int BUF = 4 * HALF;
   enum { KA0 = 0, KA1 = 1, KW0 = 2, KW1 = 3 };
-  // VMEM ops every lane issues in an epilogue after its last wait: 16 output stores (+ 1 LN-partial store)
-  constexpr int E = EPI == EPI_RES ? 17 : 16;
+  // VMEM ops every lane issues in an epilogue after its last wait: 16 output stores (+ 1 LN-partial store; MXO:
+  // 16 fp8 row stores + 4 scale-byte stores)
+  constexpr int E = EPI == EPI_RES ? 17 : MXO ? 20 : 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1381,7 +1385,10 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
     ra2 = make_rsrc(A2 + (size_t)m0_ * p.lda1, (long long)(p.M - m0_) * p.lda1 * 2);
     rw = make_rsrc(p.W + (size_t)n0_ * ldw, (long long)(p.N - n0_ - 1) * ldw * 2 + (long long)p.K * 2);
   };
-  const __amdgpu_buffer_rsrc_t rout = make_rsrc(p.out_bf16, (long long)p.M * p.ldo * 2);
+  const __amdgpu_buffer_rsrc_t rout =
+      MXO ? make_rsrc(p.out_fp8, (long long)p.M * p.ldo8) : make_rsrc(p.out_bf16, (long long)p.M * p.ldo * 2);
+  const __amdgpu_buffer_rsrc_t rsc =
+      make_rsrc(MXO ? (const void*)p.out_scale : (const void*)p.W, MXO ? (long long)((p.N + 127) >> 7) * p.out_scale_ld * 4 : 0);
   const __amdgpu_buffer_rsrc_t rres = make_rsrc(EPI == EPI_RES && p.accumulate ? p.res_in : p.out_bf16,
                                                 EPI == EPI_RES && p.accumulate ? (long long)p.M * p.ldri * 2 : 0);
   const bool ln = epi_rowout(EPI) && p.ln_stats != nullptr;
@@ -1584,6 +1591,7 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
     }
 
     if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
+      unsigned e8[16];   // MXO: E8M0 scale of block (qi, mi, qj) at [qi * 8 + mi * 2 + qj]
 #pragma unroll
       for (int qi = 0; qi < 2; ++qi)
 #pragma unroll
@@ -1607,14 +1615,60 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
               u[ni][0] = pack_bf16x2(v[0], v[1]);
               u[ni][1] = pack_bf16x2(v[2], v[3]);
             }
-            pl16swap(u[0][0], u[1][0]);
-            pl16swap(u[0][1], u[1][1]);
-            const int n = n0 + qj * 128 + wn * 32 + offg;
-            const unsigned off = (m < p.M && n < p.N && !(p.dbg_tile0 & 32)) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
-            __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)u[0][0], (int)u[0][1], (int)u[1][0], (int)u[1][1]},
-                                                   rout, (int)off, 0, 0);
+            if constexpr (MXO) {
+              // MXFP8 of the bf16-rounded values (as gemm8d's staged epilogue): the 32-column block qj*128 + wn*32
+              // of row m is fragments ni 0/1 of the 4 lane rows g4, so its |max| is the lane's 8 values reduced
+              // over l ^ 16, l ^ 32; after the quantisation a permlane16 swap gives every lane 8 consecutive bytes
+              const float f[8] = {bf16lo(u[0][0]), bf16hi(u[0][0]), bf16lo(u[0][1]), bf16hi(u[0][1]),
+                                  bf16lo(u[1][0]), bf16hi(u[1][0]), bf16lo(u[1][1]), bf16hi(u[1][1])};
+              float am = 0.f;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(f[j]));
+              const auto a32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(am), __float_as_uint(am), false, false);
+              am = fmaxf(__uint_as_float(a32[0]), __uint_as_float(a32[1]));
+              const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(am), __float_as_uint(am), false, false);
+              am = fmaxf(__uint_as_float(a16[0]), __uint_as_float(a16[1]));
+              const unsigned bits = __float_as_uint(am * (1.0f / 448.0f));
+              unsigned e = (bits >> 23) & 0xffu;
+              e += (bits & 0x7fffffu) ? 1u : 0u;
+              e = e > 254u ? 254u : e;
+              const float inv = __uint_as_float((254u - e) << 23);   // 2^(127 - e)
+              int w0 = 0, w1 = 0;
+              w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[0] * inv, f[1] * inv, w0, false);
+              w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[2] * inv, f[3] * inv, w0, true);
+              w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4] * inv, f[5] * inv, w1, false);
+              w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6] * inv, f[7] * inv, w1, true);
+              unsigned q0 = (unsigned)w0, q1 = (unsigned)w1;
+              pl16swap(q0, q1);
+              e8[qi * 8 + mi * 2 + qj] = e;
+              const int n = n0 + qj * 128 + wn * 32 + offg;
+              const unsigned off = (m < p.M && n < p.N && !(p.dbg_tile0 & 32)) ? (unsigned)m * (unsigned)p.ldo8 + (unsigned)n : OOB;
+              __builtin_amdgcn_raw_buffer_store_b64(i32x2{(int)q0, (int)q1}, rout, (int)off, 0, 0);
+            } else {
+              pl16swap(u[0][0], u[1][0]);
+              pl16swap(u[0][1], u[1][1]);
+              const int n = n0 + qj * 128 + wn * 32 + offg;
+              const unsigned off = (m < p.M && n < p.N && !(p.dbg_tile0 & 32)) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
+              __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)u[0][0], (int)u[0][1], (int)u[1][0], (int)u[1][1]},
+                                                     rout, (int)off, 0, 0);
+            }
           }
         }
+      if constexpr (MXO) {
+        // scale bytes: block (row m, 32 columns at n) -> byte ((n >> 7) * out_scale_ld + m) * 4 + ((n >> 5) & 3) =
+        // ((n0 / 128 + qj) * ld + m) * 4 + wn; the 4 lane rows hold equal scales, so store j takes block
+        // gi = j * 4 + g4 in lane row g4 (4 byte stores instead of 16)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const unsigned ev = g4 == 0 ? e8[j * 4] : g4 == 1 ? e8[j * 4 + 1] : g4 == 2 ? e8[j * 4 + 2] : e8[j * 4 + 3];
+          const int qi = j >> 1, mi = (j & 1) * 2 + (g4 >> 1), qj = g4 & 1;
+          const int m = m0 + qi * 128 + wm * 64 + mi * 16 + r16;
+          const int nb = n0 + qj * 128 + wn * 32;
+          const unsigned off = (m < p.M && nb < p.N && !(p.dbg_tile0 & 32))
+                                   ? ((unsigned)((n0 >> 7) + qj) * (unsigned)p.out_scale_ld + (unsigned)m) * 4u + (unsigned)wn : OOB;
+          __builtin_amdgcn_raw_buffer_store_b8((unsigned char)ev, rsc, (int)off, 0, 0);
+        }
+      }
     } else {   // EPI_RES
       // residual rows in the 16-byte layout (zeros out of range), all issued before the first use
       i32x4 rr[2][4][2];
@@ -2407,6 +2461,8 @@ static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream) {
     (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
     (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_GELU>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
     (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_RES>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_GELU, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
       g_num_cus = n;
@@ -2417,6 +2473,12 @@ static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream) {
   const int tn = (p.N + BN2 - 1) / BN2, tm = (p.M + BM2 - 1) / BM2;
   const int ntiles = tm * tn;
   const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
+  if (p.out_fp8) {   // fits_8s: bf16 / GELU with the MXFP8 copy as the only output
+    if (epi == EPI_BF16) hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+    else if (epi == EPI_GELU) hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL(gemm8s_kernel<EPI_BF16>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
     case EPI_GELU: hipLaunchKernelGGL(gemm8s_kernel<EPI_GELU>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
@@ -2426,12 +2488,22 @@ static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// the persistent kernel's preconditions (epilogues, no conv / batch / gather / MXFP8, K >= 256, one A stride,
-// buffer extents)
+// the persistent kernel's preconditions (epilogues, no conv / batch / gather / MXFP8 operands, K >= 256, one A
+// stride, buffer extents); an MXFP8 output only as the sole output of a bf16 / GELU epilogue (gemm_check has
+// validated its shape: N % 32, ldo8 % 16, out_scale_ld >= M)
 static bool fits_8s(const GemmArgs& p, int epi) {
   const long long lim = 0x7fffffffLL;
   if (epi != EPI_BF16 && epi != EPI_GELU && epi != EPI_RES) return false;
-  if (p.conv || p.batch > 1 || p.a_rows_per_group > 0 || p.out_fp8 || p.fp8 || p.mx_center || !p.out_bf16) return false;
+  if (p.conv || p.batch > 1 || p.a_rows_per_group > 0 || p.fp8 || p.mx_center) return false;
+  if (p.out_fp8) {
+    if (epi == EPI_RES || p.out_bf16 || !p.out_scale || p.N % 32 || p.ldo8 % 16 || p.out_scale_ld < p.M) return false;
+    if ((long long)p.M * p.ldo8 >= lim || (long long)((p.N + 127) >> 7) * p.out_scale_ld * 4 >= lim) return false;
+    if (epi == EPI_GELU && p.act) return false;
+    if (p.K < 256 || (p.A2 && p.K1 < p.K && p.lda2 != p.lda1) || (p.ln_stats && p.ln_ld > 8)) return false;
+    if (p.dbg_tile0 & 15) return false;
+    return fits_rsrc(p);
+  }
+  if (!p.out_bf16) return false;
   if (epi == EPI_GELU && p.act) return false;
   if (p.K < 256 || (p.A2 && p.K1 < p.K && p.lda2 != p.lda1) || p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15) || (p.ln_stats && p.ln_ld > 8)) return false;
   if ((long long)p.M * p.ldo * 2 >= lim) return false;

@@ -84,6 +84,50 @@ def test_mx_output_epilogue_bit_exact(lib, algo, epi, M, N, K):
     assert torch.equal(q.view(torch.uint8), rq.view(torch.uint8))
 
 
+@pytest.mark.parametrize("algo", [0, 7, 11])
+@pytest.mark.parametrize("epi,ln", [("gelu", True), ("gelu", False), ("bf16", False)])
+@pytest.mark.parametrize("M,N,K", [(5160, 4608, 1152), (300, 4608, 256), (4133, 1184, 512)])
+def test_mx_only_output_bit_exact(lib, algo, epi, ln, M, N, K):
+    """bf16-operand GEMM whose only output is the MXFP8 copy (the H/4 bf16 fc1 emitting the fc2 operand, capi.hip
+    run_block8): on the persistent kernel (algo 11, the default at these shapes) the fp8 bytes and E8M0 scales
+    are computed from registers (permlane reductions over the 4 lane rows of a 32-column block); they must equal
+    the host quantiser applied to the bf16 output of the same algo with the same epilogue (LayerNorm consumer +
+    GELU included), bit for bit -- and rows / columns past the tile edges stay untouched."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + algo)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    kw = {}
+    if ln:
+        _, st = lib.rowstats(a.float() * 1.7 + 0.3, want_bf16=False)
+        kw = dict(ln_stats=st, ln_colsum=w.float().sum(1))
+    e = lib.EPI_GELU if epi == "gelu" else lib.EPI_BF16
+    sn = (N + 127) // 128
+    q = torch.full((M, N + 32), 0x7e, device="cuda", dtype=torch.uint8)   # ldo8 = N + 32: the pad stays untouched
+    s = torch.full((sn, M + 5), -1, device="cuda", dtype=torch.int32)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    # the kernel auto-dispatch (algo 0) picks for an MXFP8 output: the persistent one from 4096 rows, else gemm8d;
+    # the bf16 reference output comes from that same kernel (the 128 tile's LayerNorm arithmetic differs)
+    ref_algo = algo if algo else (11 if M >= 4096 else 7)
+    try:
+        lib.check(lib.load().pdm_set_gemm_algo(ref_algo), "pdm_set_gemm_algo")
+        lib.gemm_ex(e, a, w, bias, out=out, **kw)
+        lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
+        lib.gemm_ex(e, a, w, bias, out_fp8=q[:, :N].view(torch.float8_e4m3fn), out_scale=s, **kw)
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+    torch.cuda.synchronize()
+    rq, rs = lib.mx_quantize(out.float())
+    assert torch.equal(q[:, :N], rq.view(torch.uint8))
+    assert bool((q[:, N:] == 0x7e).all())
+    nb = N // 32   # E8M0 bytes of the valid 32-column blocks ((kt, m) dword byte j = block kt * 4 + j)
+    got = s[:, :M].contiguous().view(torch.uint8).reshape(sn, M, 4).permute(1, 0, 2).reshape(M, sn * 4)
+    want = rs.contiguous().view(torch.uint8).reshape(sn, M, 4).permute(1, 0, 2).reshape(M, sn * 4)
+    assert torch.equal(got[:, :nb], want[:, :nb])
+    assert bool((got[:, nb:] == 0xFF).all())   # bytes of blocks past N untouched
+    assert bool((s[:, M:] == -1).all())
+
+
 @pytest.mark.parametrize("centred,offset", [(False, 0.0), (True, 0.0), (True, 2.0), (True, 8.0), (True, 32.0)])
 def test_mxfp8_layernorm_consumer_chain(lib, centred, offset):
     """fc1 of a U-ViT-H block in fp8: MX(x) operand + gamma-folded MX weight + fused LayerNorm + GELU, emitting

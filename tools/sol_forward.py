@@ -3,7 +3,7 @@ GEMM family switched off by pdm_set_gemm_tuning timing bits (wrong results, timi
 process so the variants share the box's clock state.
   a11 / a7    the forward with the persistent GEMM (algo 11, the default) / the per-tile GEMM (algo 7)
   noepi11/7   timing bit 16: every 256-tile GEMM skips its epilogue (main loops only; nothing written)
-usage: python tools/sol_forward.py [config] [rows] [rounds]"""
+usage: python tools/sol_forward.py [config] [rows] [rounds] [precision]"""
 import sys
 import time
 
@@ -16,12 +16,15 @@ from panopticdiffusionmodels_amd.utils import get_nnet  # noqa: E402
 name = sys.argv[1] if len(sys.argv) > 1 else "imagenet256_uvit_large"
 rows = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+precision = sys.argv[4] if len(sys.argv) > 4 else "bf16"
 lib = _lib.load()
 dev = torch.device("cuda")
 cfg = configs.nnet_kwargs(name)
 sd = weights.nnet_state_dict(cfg, seed=0, device=dev)
 net = get_nnet(**cfg).to(dev)
 net.load_state_dict(sd)
+if precision != "bf16":
+    net.set_precision(precision)
 zs = configs.get_config(name)["z_shape"]
 x = torch.randn(rows, *zs, device=dev)
 t = torch.rand(rows, device=dev) * 999
@@ -51,4 +54,4 @@ with torch.no_grad():
     lib.pdm_set_gemm_algo(0)
 for k, v in res.items():
     v = sorted(v)
-    print(f"{name} rows={rows} {k:8s} median {v[len(v) // 2]:.2f} ms/forward  min {v[0]:.2f}", flush=True)
+    print(f"{name} {precision} rows={rows} {k:8s} median {v[len(v) // 2]:.2f} ms/forward  min {v[0]:.2f}", flush=True)
