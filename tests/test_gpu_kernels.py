@@ -399,15 +399,22 @@ def test_attention(lib, L, Dh, q_log2):
 
 
 @pytest.mark.parametrize("algo", [1, 2, 3, 4])
-@pytest.mark.parametrize("L", [17, 66, 129, 257, 258, 334, 513, 590])
-def test_attention_algos(lib, algo, L):
+@pytest.mark.parametrize("L", [17, 32, 64, 66, 128, 129, 257, 258, 334, 513, 590])
+@pytest.mark.parametrize("ramp", [False, True])
+def test_attention_algos(lib, algo, L, ramp):
     """Both attention structures (1: streamed K/V per 64-query block; 2/3: head-resident K/V, 2 or 3 query
     tiles per wave; 4: head-resident v2, a ragged last tile at nqt = k NW + 1 (L = 66, 129, 257, 258, 513) run as the
-    third tile of a pass) at Dh = 64 on ragged lengths (the head-resident path declines shapes it cannot hold)."""
+    third tile of a pass) at Dh = 64 on ragged lengths and whole 64-key blocks (the head-resident path declines shapes
+    it cannot hold).  ramp: key magnitudes
+    grow along the sequence, so later key blocks raise the running max past the deferred-rescale threshold."""
     H, B, Dh = 4, 3, 64
     D = H * Dh
     g = torch.Generator(device="cuda").manual_seed(L + algo)
-    qkv = (torch.randn(B * L, 3 * D, device="cuda", generator=g) * 1.5).bfloat16()
+    qkv = torch.randn(B * L, 3 * D, device="cuda", generator=g) * 1.5
+    if ramp:
+        pos = torch.arange(B * L, device="cuda") % L
+        qkv[:, D:2 * D] *= (1 + 5 * pos / L)[:, None]
+    qkv = qkv.bfloat16()
     lib.check(lib.load().pdm_set_attention_algo(algo), "pdm_set_attention_algo")
     try:
         out = lib.attention(qkv, B, L, H, Dh)
