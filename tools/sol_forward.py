@@ -4,6 +4,7 @@ process so the variants share the box's clock state.
   a11 / a7    the forward with the persistent GEMM (algo 11, the default) / the per-tile GEMM (algo 7)
   noepi11/7   timing bit 16: every 256-tile GEMM skips its epilogue (main loops only; nothing written)
 usage: python tools/sol_forward.py [config] [rows] [rounds] [precision]"""
+import os
 import sys
 import time
 
@@ -34,6 +35,8 @@ if cfg["name"] == "uvit_t2i":
 else:
     extra = (torch.randint(0, 1000, (rows,), device=dev) if cfg.get("num_classes", -1) > 0 else None,)
 modes = {"a11": (11, 0), "a7": (7, 0), "noepi11": (11, 16), "noepi7": (7, 16)}
+if os.environ.get("SOL_MODES"):   # e.g. "a11:11:0,a12:12:0" = name:algo:timing bits
+    modes = {m.split(":")[0]: (int(m.split(":")[1]), int(m.split(":")[2])) for m in os.environ["SOL_MODES"].split(",")}
 res = {k: [] for k in modes}
 with torch.no_grad():
     for _ in range(20):
