@@ -218,6 +218,17 @@ def main():
     roof = gemm_roofline(prof, ncfg, 2 * B if t2i or sampler.cfg else B, precision, config=args.config)
     samp_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
+    if roof and roof.get("flops_per_forward"):
+        # the timed configuration itself (two concurrent lanes of half the rows, graph replay) has overlapping
+        # kernels whose durations are not rates; this bounds the GEMM family's rate there from below
+        gemm_tf = roof["flops_per_forward"] * sampler.nfe / 1e12
+        rate = gemm_tf / (samp_ms / 1e3)
+        roof["timed_config"] = {
+            "lanes": sampler.lanes, "gemm_tflop_per_step": round(gemm_tf, 2), "sample_ms_per_step": round(samp_ms, 2),
+            "gemm_rate_lower_bound_tflops": round(rate, 1), "frac_lower_bound": round(rate / roof["peak"], 4),
+            "note": "every GEMM FLOP of one timed step's sampling / that step's whole sampling time (attention, small "
+                    "kernels and launch gaps counted as GEMM time): a lower bound on the GEMM family's rate in the "
+                    "timed lanes configuration"}
 
     images = world * B * args.steps
     value = images / elapsed
