@@ -203,6 +203,10 @@ typedef struct pdm_gemm_args {
   const float* res_f32; int ldrf;
 } pdm_gemm_args;
 int pdm_gemm(const pdm_gemm_args* a, int epi, void* stream);
+/* Two GEMMs with the same epilogue, N, K and strides (different operands, rows and outputs) as ONE grouped launch of
+ * the persistent kernel where it takes both (the t2i image- and mask-stream Linears of a layer), else the two
+ * launches in order; results identical to two pdm_gemm calls either way. */
+int pdm_gemm_pair(const pdm_gemm_args* a, const pdm_gemm_args* b, int epi, void* stream);
 /* sizeof(pdm_gemm_args) as compiled into the library (binding layout check) */
 int pdm_gemm_args_size(void);
 /* Implicit-GEMM conv3x3 (stride 1, pad 1) on NHWC bf16 input [B, H>>up, W>>up, Cin] (up = 1: the nearest-x2

@@ -103,6 +103,8 @@ _SIGS = {
                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_void_p]),
     "pdm_gemm": (ctypes.c_int, [ctypes.POINTER(PdmGemmArgs), ctypes.c_int, ctypes.c_void_p]),
+    "pdm_gemm_pair": (ctypes.c_int, [ctypes.POINTER(PdmGemmArgs), ctypes.POINTER(PdmGemmArgs), ctypes.c_int,
+                                     ctypes.c_void_p]),
     "pdm_gemm_bf16_ln": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -324,12 +326,24 @@ def mx_quantize_gpu(x):
     return q, s
 
 
-def gemm_ex(epi, a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=None, accumulate=False,
-            ln_stats=None, ln_colsum=None, stats_out=None, out_fp8=None, out_scale=None, eps=1e-5,
-            mx_center=False, ln_gcol=None, res_in=None, res_f32=None, a2=None):
+def gemm_ex(epi, a, w, bias=None, **kw):
     """pdm_gemm with every option (include/pdm.h pdm_gemm_args).  a / w are bf16, or float8_e4m3fn with their
     scale dword arrays (MXFP8); a2 (bf16) continues a along K (the split-K skip_linear operand)."""
-    lib = load()
+    g = _gemm_args(a, w, bias, **kw)
+    check(load().pdm_gemm(ctypes.byref(g), epi, stream_ptr(a.device)), "pdm_gemm")
+
+
+def gemm_pair(epi, first, second):
+    """pdm_gemm_pair: two GEMMs of one epilogue / N / K given as gemm_ex keyword dicts (a, w, bias, ...), grouped
+    into one persistent launch where the kernel takes both."""
+    ga, gb = _gemm_args(**first), _gemm_args(**second)
+    check(load().pdm_gemm_pair(ctypes.byref(ga), ctypes.byref(gb), epi, stream_ptr(first["a"].device)),
+          "pdm_gemm_pair")
+
+
+def _gemm_args(a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=None, accumulate=False,
+               ln_stats=None, ln_colsum=None, stats_out=None, out_fp8=None, out_scale=None, eps=1e-5,
+               mx_center=False, ln_gcol=None, res_in=None, res_f32=None, a2=None):
     require_gpu(a)
     M, K = a.shape
     N = w.shape[0]
@@ -364,7 +378,7 @@ def gemm_ex(epi, a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=
         g.res_in, g.ldri = res_in.data_ptr(), res_in.stride(0)
     if res_f32 is not None:
         g.res_f32, g.ldrf = res_f32.data_ptr(), res_f32.stride(0)
-    check(lib.pdm_gemm(ctypes.byref(g), epi, stream_ptr(a.device)), "pdm_gemm")
+    return g
 
 
 def mx_quantize_centred(x, stats):

@@ -147,6 +147,10 @@ struct Workspace {
   bf16* MB;     // [rows*Lm, D] bf16 mask-stream block input (bf16 residual stream: MX is then only assembly scratch)
   bf16* SKM;    // [nhalf][rows*Lm, D]
   float* STM;   // [rows*Lm, T] LayerNorm partials of the mask stream
+  // t2i on the bf16 stream: the image block's own scratch, so it runs in lockstep with the mask block of its layer
+  // (every block Linear of the pair one grouped launch, run_block16_pair)
+  bf16 *XT2, *QKV2, *ATT2, *MLP2;
+  float* STT2;
   // fp8 forward (cfg.fp8): MXFP8 operands of the block Linears, e4m3 rows + E8M0 scale dwords [K/128][rows*Lx]
   Q8 xq;             // block input x (from the token assembly row pass)                 [rows*Lx, D]
   Q8 xtq;            // block-internal x (skip_linear / proj epilogues: qkv / fc1 operand) [rows*Lx, D]
@@ -205,6 +209,13 @@ Workspace layout(const pdm_uvit* h, int rows, char* base) {
     w.MXIN = (bf16*)take(Mm * D * 2);
     w.STM = (float*)take(Mm * T * 8);
     w.SKM = (bf16*)take((size_t)h->nhalf * Mm * D * 2);
+    if (h->res16() && !f8) {
+      w.XT2 = (bf16*)take(Mx * D * 2);
+      w.STT2 = (float*)take(Mx * T * 8);
+      w.QKV2 = (bf16*)take(Mx * 3 * D * 2);
+      w.ATT2 = (bf16*)take(Mx * D * 2);
+      w.MLP2 = (bf16*)take(Mx * h->Hid * 2);
+    }
   }
   w.bytes = off;
   return w;
@@ -255,6 +266,50 @@ int gemm(const Ctx& c, const bf16* A, int lda, const bf16* W, const float* bias,
   a.accumulate = accumulate;
   a.a_rows_per_group = a_rpg; a.a_group_stride = a_gs;
   return launch_gemm(c, a, epi);
+}
+
+// GemmArgs of a bf16 block Linear: the fused-LayerNorm consumer (ln.st_in, bf16 / GELU epilogue) or the bf16 residual
+// epilogue (EPI_RES: out = bf16(A W^T + bias (+ res_in)), partials st_out; A2 = the split-K long-skip operand)
+pdm::GemmArgs ln_args(const pdm_uvit* h, const bf16* A, const bf16* W, const float* bias, int M, int N, int K, bf16* out,
+                      const float* st_in, const float* colsum) {
+  pdm::GemmArgs a{};
+  const int T = (h->D + 255) / 256;
+  a.ln_stats = st_in; a.ln_ld = T; a.ln_D = K; a.ln_eps = 1e-5f; a.ln_colsum = colsum; a.stats_ld = T;
+  a.A1 = A; a.lda1 = K; a.K1 = K;
+  a.W = W; a.bias = bias;
+  a.M = M; a.N = N; a.K = K;
+  a.out_bf16 = out; a.ldo = N;
+  return a;
+}
+pdm::GemmArgs res_args(const bf16* A, int lda, const bf16* W, const float* bias, int M, int N, int K, const bf16* res_in,
+                       bf16* out, float* st_out, const bf16* A2 = nullptr, int lda2 = 0, int K1 = 0) {
+  pdm::GemmArgs a{};
+  a.A1 = A; a.lda1 = lda;
+  a.A2 = A2; a.lda2 = lda2;
+  a.K1 = A2 ? K1 : K;
+  a.W = W; a.bias = bias;
+  a.M = M; a.N = N; a.K = K;
+  a.out_bf16 = out; a.ldo = N;
+  a.res_in = res_in; a.ldri = N; a.accumulate = res_in ? 1 : 0;
+  a.stats_out = st_out; a.stats_ld = (N + 255) / 256;
+  return a;
+}
+
+// two GEMMs as one grouped launch where the kernel takes both (pdm::gemm_launch_pair), with the profiling hook
+// counting the pair as one launch of their summed FLOPs
+int launch_gemm_pair(const Ctx& c, const pdm::GemmArgs& a, const pdm::GemmArgs& b, int epi) {
+  PDM_CHECK(pdm::gemm_check(a, epi));
+  PDM_CHECK(pdm::gemm_check(b, epi));
+  const pdm_uvit* h = c.h;
+  const bool prof = h->prof_on && 2 * (h->prof_n + 1) <= (int)h->prof_ev.size();
+  if (prof) PDM_HIP(hipEventRecord(h->prof_ev[2 * h->prof_n], c.s));
+  PDM_HIP(pdm::gemm_launch_pair(a, b, epi, c.s));
+  if (prof) {
+    PDM_HIP(hipEventRecord(h->prof_ev[2 * h->prof_n + 1], c.s));
+    h->prof_flops[h->prof_n] = 2.0 * a.M * a.N * a.K + 2.0 * b.M * b.N * b.K;
+    ++h->prof_n;
+  }
+  return PDM_OK;
 }
 
 // MXFP8 block Linear (cfg.fp8): A and the weight `wkey` (+ "<wkey>_scale") on the block-scaled MFMA; the
@@ -411,6 +466,75 @@ int run_block16(const Ctx& c, const std::string& pre, int nseq, int L, const bf1
   // x += fc2(h) -> xout
   PDM_TRY(gemm_res(c, w.MLP, h->Hid, h->w(pre + ".mlp.fc2.weight"), h->f(pre + ".mlp.fc2.bias"), M, D, h->Hid, w.XT,
                    xout, st_out));
+  return PDM_OK;
+}
+
+// One block of each t2i stream in lockstep on the bf16 residual stream (run_block16's sequence): every Linear of the
+// two blocks (same D / Hid, different weights, rows and buffers) is one grouped launch, attention runs per stream.
+// The t2i layer's image (L = 334) and mask (L = 590) blocks are independent given x, and each alone launches under
+// one wave of 256-row tiles at the bench's rows (t2i B = 32 per GPU as two lanes: 84 / 148 tiles for N = 512).
+struct BlockIO {
+  std::string pre;
+  int L;
+  const bf16* xin;
+  const float* st_in;
+  const bf16* skip_in;
+  bf16* xout;
+  float* st_out;
+  bf16 *XT, *QKV, *ATT, *MLP;
+  float* STT;
+};
+int run_block16_pair(const Ctx& c, int nseq, const BlockIO& A, const BlockIO& B) {
+  const pdm_uvit* h = c.h;
+  const int D = h->D;
+  const int Ma = nseq * A.L, Mb = nseq * B.L;
+  const bf16* xa = A.xin;
+  const bf16* xb = B.xin;
+  const float* sa = A.st_in;
+  const float* sb = B.st_in;
+  if (A.skip_in || B.skip_in) {   // x = skip_linear(cat([x, skip], -1)); both streams have long skips or neither
+    if (!A.skip_in || !B.skip_in) return fail(PDM_ERR_STATE, "run_block16_pair: long skip in one stream only");
+    PDM_TRY(launch_gemm_pair(c,
+        res_args(A.xin, D, h->w(A.pre + ".skip_linear.weight"), h->f(A.pre + ".skip_linear.bias"), Ma, D, 2 * D, nullptr,
+                 A.XT, A.STT, A.skip_in, D, D),
+        res_args(B.xin, D, h->w(B.pre + ".skip_linear.weight"), h->f(B.pre + ".skip_linear.bias"), Mb, D, 2 * D, nullptr,
+                 B.XT, B.STT, B.skip_in, D, D),
+        pdm::EPI_RES));
+    xa = A.XT; sa = A.STT;
+    xb = B.XT; sb = B.STT;
+  }
+  PDM_TRY(launch_gemm_pair(c,   // qkv = norm1(x) W^T
+      ln_args(h, xa, h->w(A.pre + ".attn.qkv.weight"), h->f(A.pre + ".attn.qkv.ln_bias"), Ma, 3 * D, D, A.QKV, sa,
+              h->f(A.pre + ".attn.qkv.ln_colsum")),
+      ln_args(h, xb, h->w(B.pre + ".attn.qkv.weight"), h->f(B.pre + ".attn.qkv.ln_bias"), Mb, 3 * D, D, B.QKV, sb,
+              h->f(B.pre + ".attn.qkv.ln_colsum")),
+      pdm::EPI_BF16));
+  for (const BlockIO* io : {&A, &B}) {
+    pdm::AttentionArgs a{};
+    a.qkv = io->QKV; a.ldq = 3 * D;
+    a.out = io->ATT; a.ldo = D;
+    a.B = nseq; a.L = io->L; a.H = h->H; a.Dh = h->Dh;
+    a.scale = 1.0f / sqrtf((float)h->Dh);
+    a.q_log2 = 1;
+    PDM_CHECK(pdm::attention_check(a));
+    PDM_HIP(pdm::attention_launch(a, c.s));
+  }
+  PDM_TRY(launch_gemm_pair(c,   // x += proj(attn) -> XT
+      res_args(A.ATT, D, h->w(A.pre + ".attn.proj.weight"), h->f(A.pre + ".attn.proj.bias"), Ma, D, D, xa, A.XT, A.STT),
+      res_args(B.ATT, D, h->w(B.pre + ".attn.proj.weight"), h->f(B.pre + ".attn.proj.bias"), Mb, D, D, xb, B.XT, B.STT),
+      pdm::EPI_RES));
+  PDM_TRY(launch_gemm_pair(c,   // h = GELU(fc1(norm2(x)))
+      ln_args(h, A.XT, h->w(A.pre + ".mlp.fc1.weight"), h->f(A.pre + ".mlp.fc1.ln_bias"), Ma, h->Hid, D, A.MLP, A.STT,
+              h->f(A.pre + ".mlp.fc1.ln_colsum")),
+      ln_args(h, B.XT, h->w(B.pre + ".mlp.fc1.weight"), h->f(B.pre + ".mlp.fc1.ln_bias"), Mb, h->Hid, D, B.MLP, B.STT,
+              h->f(B.pre + ".mlp.fc1.ln_colsum")),
+      pdm::EPI_GELU));
+  PDM_TRY(launch_gemm_pair(c,   // x += fc2(h) -> xout
+      res_args(A.MLP, h->Hid, h->w(A.pre + ".mlp.fc2.weight"), h->f(A.pre + ".mlp.fc2.bias"), Ma, D, h->Hid, A.XT, A.xout,
+               A.st_out),
+      res_args(B.MLP, h->Hid, h->w(B.pre + ".mlp.fc2.weight"), h->f(B.pre + ".mlp.fc2.bias"), Mb, D, h->Hid, B.XT, B.xout,
+               B.st_out),
+      pdm::EPI_RES));
   return PDM_OK;
 }
 
@@ -692,27 +816,40 @@ int t2i_two_stream16(const Ctx& c, const Workspace& w, int rows, int use_ground_
   // whose output stays in XT (its proj / fc2 update XT in place), then the injection writes the layer's x.  The
   // mask block's fc2 writes its output's partials into STM (the next refresh keeps the mask rows' ones); the
   // image block's are not needed (the injection produces x's).
+  // the mask block and the image block of a layer: paired (one grouped launch per Linear) when the image stream has
+  // its own scratch (the image block's output then lives in XT2 instead of XT), else one after the other
+  const bool pair = w.XT2 != nullptr;
+  bf16* ximg = pair ? w.XT2 : w.XT;   // the image block's output (the injection's residual)
+  auto blocks = [&](const std::string& mpre, const std::string& ipre, const bf16* skm, const bf16* sk, const bf16* xin,
+                    bf16* mout) -> int {
+    if (pair) {
+      const BlockIO mio{mpre, Lm, w.MB, w.STM, skm, mout, w.STM, w.XT, w.QKV, w.ATT, w.MLP, w.STT};
+      // the image block's fc2 partials are not needed (the injection produces x's); they land in its scratch STT2
+      // so both fc2s take the same epilogue and group
+      const BlockIO iio{ipre, Lx, xin, w.ST, sk, w.XT2, w.STT2, w.XT2, w.QKV2, w.ATT2, w.MLP2, w.STT2};
+      return run_block16_pair(c, rows, mio, iio);
+    }
+    PDM_TRY(run_block16(c, mpre, rows, Lm, w.MB, w.STM, skm, mout, w.STM, w));
+    return run_block16(c, ipre, rows, Lx, xin, w.ST, sk, w.XT, nullptr, w);
+  };
   for (int i = 0; i < n; ++i, ++layer) {
     PDM_TRY(refresh(x, m));
-    PDM_TRY(run_block16(c, "in_blocks_mask." + std::to_string(i), rows, Lm, w.MB, w.STM, nullptr, w.SKM + i * MDm,
-                        w.STM, w));
-    PDM_TRY(run_block16(c, "in_blocks." + std::to_string(i), rows, Lx, x, w.ST, nullptr, w.XT, nullptr, w));
-    PDM_TRY(inject(layer, w.SKM + i * MDm, w.XT, w.SK + i * MDx));
+    PDM_TRY(blocks("in_blocks_mask." + std::to_string(i), "in_blocks." + std::to_string(i), nullptr, nullptr, x,
+                   w.SKM + i * MDm));
+    PDM_TRY(inject(layer, w.SKM + i * MDm, ximg, w.SK + i * MDx));
     x = w.SK + i * MDx;
     m = w.SKM + i * MDm;
   }
   PDM_TRY(refresh(x, m));
-  PDM_TRY(run_block16(c, "mid_block_mask", rows, Lm, w.MB, w.STM, nullptr, w.MXB, w.STM, w));
-  PDM_TRY(run_block16(c, "mid_block", rows, Lx, x, w.ST, nullptr, w.XT, nullptr, w));
-  PDM_TRY(inject(layer, w.MXB, w.XT, w.XB));
+  PDM_TRY(blocks("mid_block_mask", "mid_block", nullptr, nullptr, x, w.MXB));
+  PDM_TRY(inject(layer, w.MXB, ximg, w.XB));
   ++layer;
   for (int i = 0; i < n; ++i, ++layer) {
     PDM_TRY(refresh(w.XB, w.MXB));
     const bf16* skm = h->cfg.skip ? w.SKM + (n - 1 - i) * MDm : nullptr;
-    PDM_TRY(run_block16(c, "out_blocks_mask." + std::to_string(i), rows, Lm, w.MB, w.STM, skm, w.MXB, w.STM, w));
     const bf16* sk = h->cfg.skip ? w.SK + (n - 1 - i) * MDx : nullptr;
-    PDM_TRY(run_block16(c, "out_blocks." + std::to_string(i), rows, Lx, w.XB, w.ST, sk, w.XT, nullptr, w));
-    PDM_TRY(inject(layer, w.MXB, w.XT, w.XB));
+    PDM_TRY(blocks("out_blocks_mask." + std::to_string(i), "out_blocks." + std::to_string(i), skm, sk, w.XB, w.MXB));
+    PDM_TRY(inject(layer, w.MXB, ximg, w.XB));
   }
   // heads (477-519): noise from norm(x) patch tokens; mask head on the un-normalised m (the last mask output)
   if (use_ground_truth) {
@@ -1124,8 +1261,7 @@ int pdm_rowstats(const float* x, int ldx, int rows, int D, void* xb, float* stat
   return PDM_OK;
 }
 
-int pdm_gemm(const pdm_gemm_args* g, int epi, void* stream) {
-  if (!g) return fail(PDM_ERR_ARG, "pdm_gemm: null args");
+static pdm::GemmArgs to_gemm_args(const pdm_gemm_args* g) {
   pdm::GemmArgs a{};
   a.A1 = (const bf16*)g->A1; a.lda1 = g->lda1;
   a.A2 = (const bf16*)g->A2; a.lda2 = g->lda2;
@@ -1144,8 +1280,23 @@ int pdm_gemm(const pdm_gemm_args* g, int epi, void* stream) {
   a.mx_center = g->mx_center; a.ln_gcol = (const bf16*)g->ln_gcol;
   a.res_in = (const bf16*)g->res_in; a.ldri = g->ldri;
   a.res_f32 = g->res_f32; a.ldrf = g->ldrf;
+  return a;
+}
+
+int pdm_gemm(const pdm_gemm_args* g, int epi, void* stream) {
+  if (!g) return fail(PDM_ERR_ARG, "pdm_gemm: null args");
+  const pdm::GemmArgs a = to_gemm_args(g);
   PDM_CHECK(pdm::gemm_check(a, epi));
   PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
+  return PDM_OK;
+}
+
+int pdm_gemm_pair(const pdm_gemm_args* ga, const pdm_gemm_args* gb, int epi, void* stream) {
+  if (!ga || !gb) return fail(PDM_ERR_ARG, "pdm_gemm_pair: null args");
+  const pdm::GemmArgs a = to_gemm_args(ga), b = to_gemm_args(gb);
+  PDM_CHECK(pdm::gemm_check(a, epi));
+  PDM_CHECK(pdm::gemm_check(b, epi));
+  PDM_HIP(pdm::gemm_launch_pair(a, b, epi, (hipStream_t)stream));
   return PDM_OK;
 }
 

@@ -1331,8 +1331,41 @@ __device__ __forceinline__ void pl16swap(unsigned& a, unsigned& b) {
 
 // MXO = 1 (bf16 / GELU only): the output is the MXFP8 copy alone (out_fp8 + out_scale, no bf16 rows): the H/4 bf16
 // fc1 whose GELU epilogue emits the fp8 fc2 operand (capi.hip run_block8)
-template <int EPI, int MXO = 0>
-__global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n, int ntiles) {
+// Grouped launch (nt0 < ntiles): tiles [0, nt0) are problem p, [nt0, ntiles) problem p2 -- two GEMMs of the same
+// N / K / epilogue whose operands, rows and outputs differ (the t2i image- and mask-stream block Linears of one layer,
+// capi.hip run_block16_pair), walked as one tile list so a layer's two small launches fill the CUs together.  Every
+// per-problem field is read through the tile's view (TV); the shared ones (N, K, strides, flags) come from p.
+struct TV {
+  const bf16* A1;
+  const bf16* A2;
+  const bf16* W;
+  const float* bias;
+  const float* ln_stats;
+  const float* ln_colsum;
+  bf16* out;
+  const bf16* res;
+  float* st;
+  int M;
+};
+__device__ __forceinline__ TV tile_view(const GemmArgs& p, const GemmArgs& p2, bool second) {
+  TV v;
+  v.A1 = second ? p2.A1 : p.A1;
+  v.A2 = second ? (p2.A2 ? p2.A2 : p2.A1) : (p.A2 ? p.A2 : p.A1);
+  v.W = second ? p2.W : p.W;
+  v.bias = second ? p2.bias : p.bias;
+  v.ln_stats = second ? p2.ln_stats : p.ln_stats;
+  v.ln_colsum = second ? p2.ln_colsum : p.ln_colsum;
+  v.out = second ? p2.out_bf16 : p.out_bf16;
+  v.res = second ? p2.res_in : p.res_in;
+  v.st = second ? p2.stats_out : p.stats_out;
+  v.M = second ? p2.M : p.M;
+  return v;
+}
+
+// GRP = 1: the grouped instantiation (a second problem p2 from tile nt0 on); GRP = 0 compiles the one-problem kernel
+// with every view resolved to p at compile time (the grouped form's per-tile selects cost the L/2 forward 1.4 %)
+template <int EPI, int MXO = 0, int GRP = 0>
+__global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n, int ntiles, GemmArgs p2, int nt0) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_RES, "persistent kernel epilogues");
   static_assert(!MXO || EPI != EPI_RES, "MXFP8 output: bf16 / GELU epilogues");
   constexpr int ROWB = 128;
@@ -1357,9 +1390,11 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
   const int nx = (G >> 3) + (x < (G & 7) ? 1 : 0);
   const int ntl = tcnt > jw ? (tcnt - jw + nx - 1) / nx : 0;
   if (ntl == 0) return;
-  const int tiles_m = (p.M + BM2 - 1) / BM2;
-  auto tile_mn = [&](int i, int& m0_, int& n0_) {
-    const int u = tstart + jw + i * nx;
+  auto tile_mn = [&](int i, int& m0_, int& n0_, bool& second) {
+    int u = tstart + jw + i * nx;
+    second = GRP && u >= nt0;
+    if (second) u -= nt0;
+    const int tiles_m = ((second ? p2.M : p.M) + BM2 - 1) / BM2;
     int tm, tn;
     if (p.raster > 0) {
       const int grp = u / (p.raster * tiles_n);
@@ -1378,23 +1413,24 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
   // operand descriptors of one tile, based at its first row / column: rows past M (N) lie past num_records and
   // come back as zeros, so the per-lane offsets below are the same for every tile
   const int ldw = p.ldw > 0 ? p.ldw : p.K;
-  const bf16* A2 = p.A2 ? p.A2 : p.A1;
   __amdgpu_buffer_rsrc_t ra1, ra2, rw;
-  auto set_tile = [&](int m0_, int n0_) {
-    ra1 = make_rsrc(p.A1 + (size_t)m0_ * p.lda1, (long long)(p.M - m0_) * p.lda1 * 2);
-    ra2 = make_rsrc(A2 + (size_t)m0_ * p.lda1, (long long)(p.M - m0_) * p.lda1 * 2);
-    rw = make_rsrc(p.W + (size_t)n0_ * ldw, (long long)(p.N - n0_ - 1) * ldw * 2 + (long long)p.K * 2);
+  auto set_tile = [&](const TV& v, int m0_, int n0_) {
+    ra1 = make_rsrc(v.A1 + (size_t)m0_ * p.lda1, (long long)(v.M - m0_) * p.lda1 * 2);
+    ra2 = make_rsrc(v.A2 + (size_t)m0_ * p.lda1, (long long)(v.M - m0_) * p.lda1 * 2);
+    rw = make_rsrc(v.W + (size_t)n0_ * ldw, (long long)(p.N - n0_ - 1) * ldw * 2 + (long long)p.K * 2);
   };
-  const __amdgpu_buffer_rsrc_t rout =
-      MXO ? make_rsrc(p.out_fp8, (long long)p.M * p.ldo8) : make_rsrc(p.out_bf16, (long long)p.M * p.ldo * 2);
+  // output / residual / partials descriptors of the current tile's problem (rebuilt per tile: scalar work)
+  __amdgpu_buffer_rsrc_t rout, rres, rst;
   const __amdgpu_buffer_rsrc_t rsc =
       make_rsrc(MXO ? (const void*)p.out_scale : (const void*)p.W, MXO ? (long long)((p.N + 127) >> 7) * p.out_scale_ld * 4 : 0);
-  const __amdgpu_buffer_rsrc_t rres = make_rsrc(EPI == EPI_RES && p.accumulate ? p.res_in : p.out_bf16,
-                                                EPI == EPI_RES && p.accumulate ? (long long)p.M * p.ldri * 2 : 0);
   const bool ln = epi_rowout(EPI) && p.ln_stats != nullptr;
   const bool stats = EPI == EPI_RES && p.stats_out != nullptr;
-  const __amdgpu_buffer_rsrc_t rst =
-      make_rsrc(stats ? (const void*)p.stats_out : (const void*)p.W, stats ? (long long)p.M * p.stats_ld * 8 : 0);
+  auto set_out = [&](const TV& v) {
+    rout = MXO ? make_rsrc(p.out_fp8, (long long)v.M * p.ldo8) : make_rsrc(v.out, (long long)v.M * p.ldo * 2);
+    rres = make_rsrc(EPI == EPI_RES && p.accumulate ? (const void*)v.res : (const void*)v.out,
+                     EPI == EPI_RES && p.accumulate ? (long long)v.M * p.ldri * 2 : 0);
+    rst = make_rsrc(stats ? (const void*)v.st : (const void*)v.W, stats ? (long long)v.M * p.stats_ld * 8 : 0);
+  };
 
   // per-lane offsets (tile relative) of this wave's two 1 KiB pieces (8 rows x 128 B) in each half (h) of A and W
   const int prow = lane >> 3, pch = lane & 7;
@@ -1423,18 +1459,18 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
   // a tile's small tables -> LDS by buffer LDS-DMA (zeros past M / N; hipcc orders LDS reads behind these without
   // draining vmcnt, unlike the global-address form): the raw LN partials of its 256 rows (contiguous in
   // ln_stats), bias, LN column sums
-  auto issue_tables = [&](int m0_, int n0_) {
+  auto issue_tables = [&](const TV& v, int m0_, int n0_) {
     if (ln) {
       const int pieces = p.ln_ld * 2;   // KiB
-      const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.ln_stats + (size_t)m0_ * p.ln_ld * 2, (long long)(p.M - m0_) * p.ln_ld * 8);
+      const __amdgpu_buffer_rsrc_t rr = make_rsrc(v.ln_stats + (size_t)m0_ * p.ln_ld * 2, (long long)(v.M - m0_) * p.ln_ld * 8);
       for (int pc = wave; pc < pieces; pc += 8)
         dma16(rr, (unsigned)(pc * 1024 + lane * 16), 0, (PDM_LDS void*)(smem + S_RAW + pc * 1024));
       if (wave == 7)
-        dma16(make_rsrc(p.ln_colsum + n0_, (long long)(p.N - n0_) * 4), (unsigned)(lane * 16), 0,
+        dma16(make_rsrc(v.ln_colsum + n0_, (long long)(p.N - n0_) * 4), (unsigned)(lane * 16), 0,
               (PDM_LDS void*)(smem + S_COL + 1024));
     }
     if (wave == 6 && p.bias)
-      dma16(make_rsrc(p.bias + n0_, (long long)(p.N - n0_) * 4), (unsigned)(lane * 16), 0, (PDM_LDS void*)(smem + S_COL));
+      dma16(make_rsrc(v.bias + n0_, (long long)(p.N - n0_) * 4), (unsigned)(lane * 16), 0, (PDM_LDS void*)(smem + S_COL));
   };
 
   bf16x8 af[4][2];
@@ -1478,10 +1514,13 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
 
   const int nk = p.K / 64;   // >= 4 (gemm_launch)
   int m0, n0;
-  tile_mn(0, m0, n0);
-  set_tile(m0, n0);
+  bool sec;
+  tile_mn(0, m0, n0, sec);
+  TV cv = tile_view(p, p2, GRP && sec), nv = cv;
+  set_tile(cv, m0, n0);
+  set_out(cv);   // one problem: the output descriptors are built once (grouped: again per tile)
   // prologue of the first tile: tables, K-tile 0, A0 W0 W1 of K-tile 1; the wait retires the tables and A0 W0 W1(0)
-  issue_tables(m0, n0);
+  issue_tables(cv, m0, n0);
   issue(0, 0, KA0);
   issue(0, 0, KW0);
   issue(0, 0, KW1);
@@ -1495,7 +1534,11 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
   for (int it = 0; it < ntl; ++it) {
     const bool has_next = it + 1 < ntl;
     int m0n = 0, n0n = 0;
-    if (has_next) tile_mn(it + 1, m0n, n0n);
+    if (has_next) {
+      bool secn;
+      tile_mn(it + 1, m0n, n0n, secn);
+      nv = tile_view(p, p2, GRP && secn);
+    }
 #pragma unroll
     for (int f = 0; f < 32; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int par = (it * nk) & 1;   // ring slot of the tile's K-tile 0
@@ -1526,7 +1569,7 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
       // phase B: quadrants (1,0) (1,1); issues A0 W0 W1 of K-tile g+2 (the next tile's from kt = nk-2 on)
       read_a(buf, 1);
       lds_done();
-      if (kt == nk - 2 && has_next) set_tile(m0n, n0n);
+      if (kt == nk - 2 && has_next) set_tile(nv, m0n, n0n);
       if (m2) {
         const int k2 = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
         issue(slot, k2, KA0);
@@ -1547,15 +1590,19 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
     if (p.dbg_tile0 & 16) {    // timing experiment: no epilogue (its E stores still issued, to nowhere)
 #pragma unroll
       for (int f = 0; f < 32; ++f) asm volatile("" ::"v"(acc[f]));
-      if (has_next) issue_tables(m0n, n0n);
+      if (has_next) issue_tables(nv, m0n, n0n);
+      if constexpr (GRP) set_out(cv);
 #pragma unroll
       for (int s = 0; s < E; ++s) __builtin_amdgcn_raw_buffer_store_b32(0, rout, (int)OOB, 0, 0);
       m0 = m0n;
       n0 = n0n;
+      cv = nv;
       continue;
     }
 
-    // ---- epilogue of tile (m0, n0) ----
+    // ---- epilogue of tile (m0, n0) of problem cv ----
+    if constexpr (GRP) set_out(cv);
+    const int M = cv.M;
     // this lane's columns: fragment (qj, ni) covers n0 + qj*128 + wn*32 + ni*16 + g4*4 + [0, 4)
     f32x4 bv[2][2], cs[2][2];
     lds_rd_cols(smem + S_COL + (wn * 32 + g4 * 4) * 4, bv, cs);
@@ -1577,7 +1624,7 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
         if (!ln) cs[qj][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     bar_raw();   // lnrow complete; the raw / column tables are free for the next tile's
-    if (has_next) issue_tables(m0n, n0n);
+    if (has_next) issue_tables(nv, m0n, n0n);
     const int offg = (g4 & 1) * 16 + (g4 >> 1) * 8;   // post-swap column offset of the lane's 8 columns
     float2 mrow[2][4];   // (mean, rstd) of the lane's 8 rows
     {
@@ -1642,13 +1689,13 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
               pl16swap(q0, q1);
               e8[qi * 8 + mi * 2 + qj] = e;
               const int n = n0 + qj * 128 + wn * 32 + offg;
-              const unsigned off = (m < p.M && n < p.N && !(p.dbg_tile0 & 32)) ? (unsigned)m * (unsigned)p.ldo8 + (unsigned)n : OOB;
+              const unsigned off = (m < M && n < p.N && !(p.dbg_tile0 & 32)) ? (unsigned)m * (unsigned)p.ldo8 + (unsigned)n : OOB;
               __builtin_amdgcn_raw_buffer_store_b64(i32x2{(int)q0, (int)q1}, rout, (int)off, 0, 0);
             } else {
               pl16swap(u[0][0], u[1][0]);
               pl16swap(u[0][1], u[1][1]);
               const int n = n0 + qj * 128 + wn * 32 + offg;
-              const unsigned off = (m < p.M && n < p.N && !(p.dbg_tile0 & 32)) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
+              const unsigned off = (m < M && n < p.N && !(p.dbg_tile0 & 32)) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
               __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)u[0][0], (int)u[0][1], (int)u[1][0], (int)u[1][1]},
                                                      rout, (int)off, 0, 0);
             }
@@ -1664,7 +1711,7 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
           const int qi = j >> 1, mi = (j & 1) * 2 + (g4 >> 1), qj = g4 & 1;
           const int m = m0 + qi * 128 + wm * 64 + mi * 16 + r16;
           const int nb = n0 + qj * 128 + wn * 32;
-          const unsigned off = (m < p.M && nb < p.N && !(p.dbg_tile0 & 32))
+          const unsigned off = (m < M && nb < p.N && !(p.dbg_tile0 & 32))
                                    ? ((unsigned)((n0 >> 7) + qj) * (unsigned)p.out_scale_ld + (unsigned)m) * 4u + (unsigned)wn : OOB;
           __builtin_amdgcn_raw_buffer_store_b8((unsigned char)ev, rsc, (int)off, 0, 0);
         }
@@ -1680,7 +1727,7 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
 #pragma unroll
           for (int qj = 0; qj < 2; ++qj) {
             const int m = m0 + qi * 128 + wm * 64 + mi * 16 + r16, n = n0 + qj * 128 + wn * 32 + offg;
-            const unsigned off = (acc_res && m < p.M && n < p.N && !(p.dbg_tile0 & 64))
+            const unsigned off = (acc_res && m < M && n < p.N && !(p.dbg_tile0 & 64))
                                      ? ((unsigned)m * (unsigned)p.ldri + (unsigned)n) * 2u : OOB;
             rr[qi][mi][qj] = __builtin_amdgcn_raw_buffer_load_b128(rres, (int)off, 0, 0);
           }
@@ -1718,7 +1765,7 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
             pl16swap(u[0][0], u[1][0]);
             pl16swap(u[0][1], u[1][1]);
             const int n = n0 + qj * 128 + wn * 32 + offg;
-            const unsigned off = (m < p.M && n < p.N && !(p.dbg_tile0 & 32)) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
+            const unsigned off = (m < M && n < p.N && !(p.dbg_tile0 & 32)) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
             __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)u[0][0], (int)u[0][1], (int)u[1][0], (int)u[1][1]},
                                                    rout, (int)off, 0, 0);
           }
@@ -1772,12 +1819,13 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
           }
         }
         const int m = m0 + ml;
-        const unsigned off = (stats && m < p.M) ? (unsigned)((m * p.stats_ld + (n0 >> 8)) * 2 + c) * 4u : OOB;
+        const unsigned off = (stats && m < M) ? (unsigned)((m * p.stats_ld + (n0 >> 8)) * 2 + c) * 4u : OOB;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), rst, (int)off, 0, 0);
       }
     }
     m0 = m0n;
     n0 = n0n;
+    cv = nv;
   }
 }
 
@@ -2455,7 +2503,8 @@ static hipError_t launch8d(const GemmArgs& p, int epi, hipStream_t stream) {
 }
 
 static int g_num_cus = 0;
-static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream) {
+// q / nt0: the grouped launch's second problem and the first one's tile count (q = p, nt0 = all tiles: one problem)
+static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream, const GemmArgs* p2 = nullptr) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
@@ -2471,18 +2520,36 @@ static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream) {
     attr_set = true;
   }
   const int tn = (p.N + BN2 - 1) / BN2, tm = (p.M + BM2 - 1) / BM2;
-  const int ntiles = tm * tn;
+  const int nt0 = tm * tn;
+  const int ntiles = nt0 + (p2 ? (p2->M + BM2 - 1) / BM2 * tn : 0);
+  const GemmArgs& q = p2 ? *p2 : p;
   const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
   if (p.out_fp8) {   // fits_8s: bf16 / GELU with the MXFP8 copy as the only output
-    if (epi == EPI_BF16) hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
-    else if (epi == EPI_GELU) hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+    if (epi == EPI_BF16) hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, p, ntiles);
+    else if (epi == EPI_GELU) hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, p, ntiles);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
+  if (p2) {
+    static bool attr_g = false;
+    if (!attr_g) {
+      (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_GELU, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_RES, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      attr_g = true;
+    }
+    switch (epi) {
+      case EPI_BF16: hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 0, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
+      case EPI_GELU: hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 0, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
+      case EPI_RES: hipLaunchKernelGGL((gemm8s_kernel<EPI_RES, 0, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (epi) {
-    case EPI_BF16: hipLaunchKernelGGL(gemm8s_kernel<EPI_BF16>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
-    case EPI_GELU: hipLaunchKernelGGL(gemm8s_kernel<EPI_GELU>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
-    case EPI_RES: hipLaunchKernelGGL(gemm8s_kernel<EPI_RES>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
+    case EPI_BF16: hipLaunchKernelGGL(gemm8s_kernel<EPI_BF16>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
+    case EPI_GELU: hipLaunchKernelGGL(gemm8s_kernel<EPI_GELU>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
+    case EPI_RES: hipLaunchKernelGGL(gemm8s_kernel<EPI_RES>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -2547,6 +2614,23 @@ static bool fits_rsrc(const GemmArgs& p) {
   const long long a2 = p.A2 ? (long long)p.M * p.lda2 * 2 : 0;
   const long long w = (long long)p.N * (p.ldw > 0 ? p.ldw : p.K) * es;
   return a1 < lim && a2 < lim && w < lim && (!p.conv || p.convW < 4096);
+}
+
+hipError_t gemm_launch_pair(const GemmArgs& a, const GemmArgs& b, int epi, hipStream_t stream) {
+  GemmArgs p = a, q = b;
+  p.raster = q.raster = g_gemm_raster ? g_gemm_raster : (p.N >= 8 * BN2 ? 8 : 0);
+  p.dbg_tile0 = q.dbg_tile0 = g_gemm_dbg;
+  const bool algo_ok = g_gemm_algo == 0 || g_gemm_algo == 11;
+  const bool same = p.N == q.N && p.K == q.K && p.K1 == q.K1 && p.lda1 == q.lda1 && p.ldw == q.ldw && p.ldo == q.ldo &&
+                    p.ldri == q.ldri && p.accumulate == q.accumulate && p.stats_ld == q.stats_ld && p.ln_ld == q.ln_ld &&
+                    p.ln_D == q.ln_D && p.ln_eps == q.ln_eps && !p.bias == !q.bias && !p.ln_stats == !q.ln_stats &&
+                    !p.stats_out == !q.stats_out && !p.A2 == !q.A2 && (!p.A2 || p.lda2 == q.lda2) && !p.out_fp8 && !q.out_fp8;
+  // grouped only where each GEMM alone would take the persistent kernel (gemm_launch's rule), so a problem's
+  // arithmetic -- and the sampler's batch invariance -- does not depend on the other problem's rows
+  if (algo_ok && same && p.M >= 4096 && q.M >= 4096 && p.N >= 256 && fits_8s(p, epi) && fits_8s(q, epi))
+    return launch8s(p, epi, stream, &q);
+  const hipError_t e = gemm_launch(a, epi, stream);
+  return e != hipSuccess ? e : gemm_launch(b, epi, stream);
 }
 
 hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {

@@ -1,0 +1,16 @@
+#!/bin/bash
+# L/2 forward same-box A/B (HEAD lib vs this tree) after the grouped-kernel split; gemm kernel tests first.
+OUT=${GRAFT_REPO_ROOT:-.}/gpurun_out/${1:-r04q}
+mkdir -p $OUT
+stop_on_fault() { case $1 in 0|1) return 0;; *) echo "step exited $1: stopping"; exit $1;; esac; }
+timeout -k 10 600 python3 -u -m pytest -x -q -rf --timeout 300 --timeout-method thread tests/test_gpu_kernels.py -m gpu -k "gemm" > $OUT/pytest.log 2>&1
+s=$?; tail -2 $OUT/pytest.log; [ $s -ne 0 ] && exit $s
+for r in 1 2 3 4; do
+  for lib in ab/libpdm_head.so panopticdiffusionmodels_amd/libpdm.so; do
+    n=$(basename $lib .so)
+    PDM_LIB_PATH=$lib timeout -k 10 200 python3 tools/time_forward.py imagenet256_uvit_large 100 10 >> $OUT/l2_fwd_$n.log 2>&1
+    s=$?; stop_on_fault $s
+  done
+done
+grep -H ms/forward $OUT/l2_fwd_*.log
+echo done
