@@ -326,10 +326,11 @@ def mx_quantize_gpu(x):
     return q, s
 
 
-def gemm_ex(epi, a, w, bias=None, **kw):
-    """pdm_gemm with every option (include/pdm.h pdm_gemm_args).  a / w are bf16, or float8_e4m3fn with their
-    scale dword arrays (MXFP8); a2 (bf16) continues a along K (the split-K skip_linear operand)."""
-    g = _gemm_args(a, w, bias, **kw)
+def gemm_ex(epi, a, w, bias=None, *args, **kw):
+    """pdm_gemm with every option (include/pdm.h pdm_gemm_args; positional after bias: a_scale, w_scale, out, ...).
+    a / w are bf16, or float8_e4m3fn with their scale dword arrays (MXFP8); a2 (bf16) continues a along K (the
+    split-K skip_linear operand)."""
+    g = _gemm_args(a, w, bias, *args, **kw)
     check(load().pdm_gemm(ctypes.byref(g), epi, stream_ptr(a.device)), "pdm_gemm")
 
 
