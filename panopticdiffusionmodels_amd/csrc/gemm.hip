@@ -1347,25 +1347,30 @@ struct TV {
   float* st;
   int M;
 };
-__device__ __forceinline__ TV tile_view(const GemmArgs& p, const GemmArgs& p2, bool second) {
+__host__ __device__ __forceinline__ TV view_of(const GemmArgs& q) {
+  return TV{q.A1, q.A2 ? q.A2 : q.A1, q.W, q.bias, q.ln_stats, q.ln_colsum, q.out_bf16, q.res_in, q.stats_out, q.M};
+}
+// the view of a tile's problem: p's fields, or the second problem's (t2) -- a field-wise select on a small by-value
+// struct (a whole second GemmArgs bound by reference made hipcc copy both to scratch: 784 B per lane)
+__device__ __forceinline__ TV tile_view(const GemmArgs& p, const TV& t2, bool second) {
   TV v;
-  v.A1 = second ? p2.A1 : p.A1;
-  v.A2 = second ? (p2.A2 ? p2.A2 : p2.A1) : (p.A2 ? p.A2 : p.A1);
-  v.W = second ? p2.W : p.W;
-  v.bias = second ? p2.bias : p.bias;
-  v.ln_stats = second ? p2.ln_stats : p.ln_stats;
-  v.ln_colsum = second ? p2.ln_colsum : p.ln_colsum;
-  v.out = second ? p2.out_bf16 : p.out_bf16;
-  v.res = second ? p2.res_in : p.res_in;
-  v.st = second ? p2.stats_out : p.stats_out;
-  v.M = second ? p2.M : p.M;
+  v.A1 = second ? t2.A1 : p.A1;
+  v.A2 = second ? t2.A2 : (p.A2 ? p.A2 : p.A1);
+  v.W = second ? t2.W : p.W;
+  v.bias = second ? t2.bias : p.bias;
+  v.ln_stats = second ? t2.ln_stats : p.ln_stats;
+  v.ln_colsum = second ? t2.ln_colsum : p.ln_colsum;
+  v.out = second ? t2.out : p.out_bf16;
+  v.res = second ? t2.res : p.res_in;
+  v.st = second ? t2.st : p.stats_out;
+  v.M = second ? t2.M : p.M;
   return v;
 }
 
-// GRP = 1: the grouped instantiation (a second problem p2 from tile nt0 on); GRP = 0 compiles the one-problem kernel
-// with every view resolved to p at compile time (the grouped form's per-tile selects cost the L/2 forward 1.4 %)
-template <int EPI, int MXO = 0, int GRP = 0>
-__global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n, int ntiles, GemmArgs p2, int nt0) {
+// GRP = 1: the grouped kernel (a second problem p2 from tile nt0 on, gemm8g_kernel); GRP = 0 compiles the one-problem
+// kernel with every view resolved to p at compile time
+template <int EPI, int MXO, int GRP>
+__device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int ntiles, const TV& p2, int nt0) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_RES, "persistent kernel epilogues");
   static_assert(!MXO || EPI != EPI_RES, "MXFP8 output: bf16 / GELU epilogues");
   constexpr int ROWB = 128;
@@ -1394,7 +1399,7 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
     int u = tstart + jw + i * nx;
     second = GRP && u >= nt0;
     if (second) u -= nt0;
-    const int tiles_m = ((second ? p2.M : p.M) + BM2 - 1) / BM2;
+    const int tiles_m = ((GRP && second ? p2.M : p.M) + BM2 - 1) / BM2;
     int tm, tn;
     if (p.raster > 0) {
       const int grp = u / (p.raster * tiles_n);
@@ -1537,7 +1542,7 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
     if (has_next) {
       bool secn;
       tile_mn(it + 1, m0n, n0n, secn);
-      nv = tile_view(p, p2, GRP && secn);
+      if constexpr (GRP) nv = tile_view(p, p2, secn);   // one problem: nv == cv throughout
     }
 #pragma unroll
     for (int f = 0; f < 32; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1596,7 +1601,7 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
       for (int s = 0; s < E; ++s) __builtin_amdgcn_raw_buffer_store_b32(0, rout, (int)OOB, 0, 0);
       m0 = m0n;
       n0 = n0n;
-      cv = nv;
+      if constexpr (GRP) cv = nv;
       continue;
     }
 
@@ -1825,8 +1830,19 @@ __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n,
     }
     m0 = m0n;
     n0 = n0n;
-    cv = nv;
+    if constexpr (GRP) cv = nv;
   }
+}
+
+// the one-problem kernel keeps its own signature (a second by-value GemmArgs in every launch measured +0.7 % on the
+// L/2 forward); the grouped kernel takes both problems
+template <int EPI, int MXO = 0>
+__global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n, int ntiles) {
+  gemm8s_body<EPI, MXO, 0>(p, tiles_n, ntiles, TV{}, ntiles);
+}
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm8g_kernel(GemmArgs p, int tiles_n, int ntiles, TV p2, int nt0) {
+  gemm8s_body<EPI, 0, 1>(p, tiles_n, ntiles, p2, nt0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2525,31 +2541,31 @@ static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream, const
   const GemmArgs& q = p2 ? *p2 : p;
   const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
   if (p.out_fp8) {   // fits_8s: bf16 / GELU with the MXFP8 copy as the only output
-    if (epi == EPI_BF16) hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, p, ntiles);
-    else if (epi == EPI_GELU) hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, p, ntiles);
+    if (epi == EPI_BF16) hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+    else if (epi == EPI_GELU) hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
   if (p2) {
     static bool attr_g = false;
     if (!attr_g) {
-      (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
-      (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_GELU, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
-      (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_RES, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8g_kernel<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8g_kernel<EPI_GELU>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8g_kernel<EPI_RES>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
       attr_g = true;
     }
     switch (epi) {
-      case EPI_BF16: hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 0, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
-      case EPI_GELU: hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 0, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
-      case EPI_RES: hipLaunchKernelGGL((gemm8s_kernel<EPI_RES, 0, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
+      case EPI_BF16: hipLaunchKernelGGL(gemm8g_kernel<EPI_BF16>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0); break;
+      case EPI_GELU: hipLaunchKernelGGL(gemm8g_kernel<EPI_GELU>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0); break;
+      case EPI_RES: hipLaunchKernelGGL(gemm8g_kernel<EPI_RES>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }
   switch (epi) {
-    case EPI_BF16: hipLaunchKernelGGL(gemm8s_kernel<EPI_BF16>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
-    case EPI_GELU: hipLaunchKernelGGL(gemm8s_kernel<EPI_GELU>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
-    case EPI_RES: hipLaunchKernelGGL(gemm8s_kernel<EPI_RES>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, q, nt0); break;
+    case EPI_BF16: hipLaunchKernelGGL(gemm8s_kernel<EPI_BF16>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
+    case EPI_GELU: hipLaunchKernelGGL(gemm8s_kernel<EPI_GELU>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
+    case EPI_RES: hipLaunchKernelGGL(gemm8s_kernel<EPI_RES>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
