@@ -12,6 +12,7 @@ run() {   # name, args...
 for l in 1 2 3 4; do run l2_lanes$l --lanes $l; done
 run l2_b64_l2 --batch 64 --lanes 2
 run l2_b64_l4 --batch 64 --lanes 4
-for l in 2 3; do run t2i_lanes$l --config mscoco_uvit_small --lanes $l; done
+for l in 1 2 3; do run t2i_lanes$l --config mscoco_uvit_small --lanes $l; done
+run t2i_b64_l2 --config mscoco_uvit_small --batch 64 --lanes 2
 for l in 2 3; do run h4_lanes$l --config imagenet512_uvit_huge --lanes $l; done
 echo done
