@@ -20,12 +20,8 @@ import os
 import sys
 import time
 
-# HIP hardware queues of this process, set before the runtime starts: the two sampling lanes' streams, the launch
-# stream and -- under torch.distributed -- RCCL's own streams exceed HIP's default of 4, and streams past the
-# limit share a queue, which serialises the lanes (U-ViT-L/2 under torchrun at world size 1: 48 vs 58 img/s,
-# DESIGN §6).  PDM_KEEP_HW_QUEUES=1 keeps the environment's value (A/B runs).
-if os.environ.get("PDM_KEEP_HW_QUEUES") != "1" and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# HIP hardware queues: the environment's (the box's default of 4).  The sampling lanes run on high-priority streams
+# of their own queue pool (sampler.py), so they stay concurrent beside the launch stream and RCCL's.
 
 import torch
 import torch.distributed as dist

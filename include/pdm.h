@@ -50,9 +50,20 @@ int pdm_device_arch(char* buf, int len);
  *              math-only timing variants (wrong results) */
 /* GEMM tile-order knob: raster = row panels per tile group inside an XCD's tile range (0 = row-major);
  * dbg_tile0 bit 0 stages every tile's operands from tile (0, 0); bit 1 lets a bf16 GEMM run with no output (mainloop +
- * LDS staging only); bit 4 skips every 256-tile epilogue -- timing experiments, results are wrong */
+ * LDS staging only); bit 4 skips every 256-tile epilogue -- timing experiments, results are wrong; bit 7 (tests):
+ * a stream-K tail never takes its predecessor's hand-off and recomputes the tile (results unchanged) */
 int pdm_set_gemm_tuning(int raster, int dbg_tile0);
 int pdm_set_gemm_algo(int algo);
+/* stream-K policy of the persistent GEMM (the last, partly filled wave of 256 x 256 tiles spread over all CUs as
+ * K-step ranges; results bit-identical to whole tiles): 0 off (default: measured slower at every U-ViT shape,
+ * DESIGN.md §4c), 1 auto (where the last wave is < 97 % full), 2 wherever it applies; + 4: standalone pdm_gemm calls
+ * take it too, on library-owned state (one stream at a time; the forwards use their workspace's own state) */
+int pdm_set_gemm_sk(int mode);
+/* number of stream-K GEMM launches issued by this process so far (host-side count) */
+long long pdm_gemm_sk_launches(void);
+/* stream-K diagnostics gathered while pdm_set_gemm_tuning bit 8 is set: out3 = {tails run, hand-offs not taken,
+ * summed poll time in 10 ns ticks}; reading clears them (synchronises the device) */
+int pdm_gemm_sk_stats(unsigned long long* out3);
 int pdm_set_attention_algo(int algo);
 
 /* ---- network handle: libs/uvit.py:138-230 UViT, libs/uvit_t2i.py:258-525 UViT (t2i) -------------- */

@@ -74,6 +74,9 @@ _SIGS = {
     "pdm_version": (ctypes.c_int, []),
     "pdm_device_arch": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     "pdm_set_gemm_algo": (ctypes.c_int, [ctypes.c_int]),
+    "pdm_set_gemm_sk": (ctypes.c_int, [ctypes.c_int]),
+    "pdm_gemm_sk_launches": (ctypes.c_longlong, []),
+    "pdm_gemm_sk_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     "pdm_set_attention_algo": (ctypes.c_int, [ctypes.c_int]),
     "pdm_set_gemm_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "pdm_uvit_create": (ctypes.c_int, [ctypes.POINTER(PdmUvitCfg), ctypes.POINTER(ctypes.c_void_p)]),

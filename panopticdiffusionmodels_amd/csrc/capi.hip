@@ -19,6 +19,8 @@ using pdm::bf16;
 namespace {
 
 thread_local std::string g_err;
+bool g_sk_standalone = false;       // pdm_set_gemm_sk bit 2: standalone pdm_gemm calls take stream-K (library state)
+constexpr int SK_LAUNCHES = 512;    // stream-K flag blocks per forward workspace (GEMM launches of one forward)
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -156,6 +158,11 @@ struct Workspace {
   Q8 xtq;            // block-internal x (skip_linear / proj epilogues: qkv / fc1 operand) [rows*Lx, D]
   Q8 atq;            // attention output (proj operand)                                  [rows*Lx, D]
   Q8 mlq;            // GELU(fc1) (fc2 operand)                                          [rows*Lx, Hid]
+  // stream-K state of the persistent GEMM (pdm::GemmArgs::sk_flags / sk_slab): SK_LAUNCHES blocks of 256 flag words
+  // (one block per GEMM launch of a forward, zeroed at the start of every forward) + one 64 MiB accumulator slab
+  // reused by every launch (stream order)
+  unsigned* SKF;
+  float* SKS;
   size_t bytes;
 };
 
@@ -217,6 +224,8 @@ Workspace layout(const pdm_uvit* h, int rows, char* base) {
       w.MLP2 = (bf16*)take(Mx * h->Hid * 2);
     }
   }
+  w.SKF = (unsigned*)take((size_t)SK_LAUNCHES * pdm::SK_FLAG_WORDS * 4);
+  w.SKS = (float*)take((size_t)pdm::SK_SLAB_BYTES);
   w.bytes = off;
   return w;
 }
@@ -225,7 +234,23 @@ Workspace layout(const pdm_uvit* h, int rows, char* base) {
 struct Ctx {
   const pdm_uvit* h;
   hipStream_t s;
+  // stream-K state of this forward (null: whole-tile GEMMs): flag blocks handed out one per GEMM launch
+  unsigned* skf = nullptr;
+  float* sks = nullptr;
+  int* skn = nullptr;
 };
+
+// a forward's stream-K state: its flag blocks zeroed on the stream first (one memset node in a captured graph); none
+// while the policy is off (a graph captured then keeps whole tiles)
+int sk_begin(Ctx& c, const Workspace& w, int* counter) {
+  *counter = 0;
+  if (pdm::gemm_get_sk() == 0) return PDM_OK;
+  PDM_HIP(hipMemsetAsync(w.SKF, 0, (size_t)SK_LAUNCHES * pdm::SK_FLAG_WORDS * 4, c.s));
+  c.skf = w.SKF;
+  c.sks = w.SKS;
+  c.skn = counter;
+  return PDM_OK;
+}
 
 // fused-LayerNorm operands of one GEMM: partials produced (st_out) or consumed (st_in + colsum)
 struct LnIO {
@@ -239,8 +264,13 @@ int launch_gemm(const Ctx& c, const pdm::GemmArgs& a, int epi) {
   PDM_CHECK(pdm::gemm_check(a, epi));
   const pdm_uvit* h = c.h;
   const bool prof = h->prof_on && 2 * (h->prof_n + 1) <= (int)h->prof_ev.size();
+  pdm::GemmArgs b = a;
+  if (c.skf && *c.skn < SK_LAUNCHES) {   // this launch's own zeroed flag block (used only if it takes stream-K)
+    b.sk_flags = c.skf + (size_t)(*c.skn)++ * pdm::SK_FLAG_WORDS;
+    b.sk_slab = c.sks;
+  }
   if (prof) PDM_HIP(hipEventRecord(h->prof_ev[2 * h->prof_n], c.s));
-  PDM_HIP(pdm::gemm_launch(a, epi, c.s));
+  PDM_HIP(pdm::gemm_launch(b, epi, c.s));
   if (prof) {
     PDM_HIP(hipEventRecord(h->prof_ev[2 * h->prof_n + 1], c.s));
     h->prof_flops[h->prof_n] = 2.0 * a.M * a.N * a.K;
@@ -878,6 +908,21 @@ int pdm_set_gemm_algo(int algo) {
   return PDM_OK;
 }
 
+int pdm_set_gemm_sk(int mode) {
+  if ((mode & 3) > 2 || mode < 0 || mode > 7) return fail(PDM_ERR_ARG, "pdm_set_gemm_sk: mode must be 0..2 (+4)");
+  pdm::gemm_set_sk(mode & 3);
+  g_sk_standalone = (mode & 4) != 0;
+  return PDM_OK;
+}
+
+long long pdm_gemm_sk_launches(void) { return pdm::gemm_sk_launches(); }
+
+int pdm_gemm_sk_stats(unsigned long long* out3) {
+  if (!out3) return fail(PDM_ERR_ARG, "pdm_gemm_sk_stats: null output");
+  if (pdm::gemm_sk_stats(out3)) return fail(PDM_ERR_HIP, "pdm_gemm_sk_stats: device copy failed");
+  return PDM_OK;
+}
+
 int pdm_set_gemm_tuning(int raster, int dbg_tile0) {
   if (raster < 0 || raster > 64) return fail(PDM_ERR_ARG, "pdm_set_gemm_tuning: raster must be in [0, 64]");
   pdm::gemm_set_tuning(raster, dbg_tile0);
@@ -1063,6 +1108,8 @@ int pdm_uvit_forward(pdm_uvit* h, const float* x, const float* t, const int64_t*
   if (w.bytes > workspace_bytes) return fail(PDM_ERR_ARG, "pdm_uvit_forward: workspace too small");
   h->prof_n = 0;
   Ctx c{h, (hipStream_t)stream};
+  int skn = 0;
+  PDM_TRY(sk_begin(c, w, &skn));
   const int D = h->D, L = h->Lx;
   {
     pdm::AssembleArgs a{};
@@ -1104,6 +1151,8 @@ int pdm_uvit_t2i_forward(pdm_uvit* h, const float* x, const float* t, const floa
   if (w.bytes > workspace_bytes) return fail(PDM_ERR_ARG, "pdm_uvit_t2i_forward: workspace too small");
   h->prof_n = 0;
   Ctx c{h, (hipStream_t)stream};
+  int skn = 0;
+  PDM_TRY(sk_begin(c, w, &skn));
   const int D = h->D, Lx = h->Lx, Lm = h->Lm, nctx = h->cfg.num_clip_token;
   // context_embed (libs/uvit_t2i.py:387): bf16 cast + GEMM (+bias) -> fp32 context tokens
   PDM_HIP(pdm::cast_bf16_launch(context, w.CTXB, (long long)rows * nctx * h->cfg.clip_dim, c.s));
@@ -1261,6 +1310,27 @@ int pdm_rowstats(const float* x, int ldx, int rows, int D, void* xb, float* stat
   return PDM_OK;
 }
 
+// stream-K state for standalone pdm_gemm calls (pdm_set_gemm_sk mode bit 2; tests and tools, ONE stream at a time):
+// a ring of flag blocks, zeroed whenever it wraps, and one slab
+static int sk_standalone(pdm::GemmArgs& a, hipStream_t s) {
+  constexpr int RING = 4096;
+  static unsigned* flags = nullptr;
+  static float* slab = nullptr;
+  static int next = 0;
+  if (!flags) {
+    PDM_HIP(hipMalloc(&flags, (size_t)RING * pdm::SK_FLAG_WORDS * 4));
+    PDM_HIP(hipMalloc(&slab, (size_t)pdm::SK_SLAB_BYTES));
+    PDM_HIP(hipMemset(flags, 0, (size_t)RING * pdm::SK_FLAG_WORDS * 4));
+  }
+  if (next == RING) {
+    PDM_HIP(hipMemsetAsync(flags, 0, (size_t)RING * pdm::SK_FLAG_WORDS * 4, s));
+    next = 0;
+  }
+  a.sk_flags = flags + (size_t)next++ * pdm::SK_FLAG_WORDS;
+  a.sk_slab = slab;
+  return PDM_OK;
+}
+
 static pdm::GemmArgs to_gemm_args(const pdm_gemm_args* g) {
   pdm::GemmArgs a{};
   a.A1 = (const bf16*)g->A1; a.lda1 = g->lda1;
@@ -1285,8 +1355,9 @@ static pdm::GemmArgs to_gemm_args(const pdm_gemm_args* g) {
 
 int pdm_gemm(const pdm_gemm_args* g, int epi, void* stream) {
   if (!g) return fail(PDM_ERR_ARG, "pdm_gemm: null args");
-  const pdm::GemmArgs a = to_gemm_args(g);
+  pdm::GemmArgs a = to_gemm_args(g);
   PDM_CHECK(pdm::gemm_check(a, epi));
+  if (g_sk_standalone) PDM_TRY(sk_standalone(a, (hipStream_t)stream));
   PDM_HIP(pdm::gemm_launch(a, epi, (hipStream_t)stream));
   return PDM_OK;
 }

@@ -11,6 +11,7 @@
 // with an XOR swizzle (chunk ^ ((row >> 1) & 7)) applied on the SOURCE address, which makes every
 // ds_read_b128 fragment read bank-conflict free.  The MFMA is issued with the weight fragment as the A
 // operand so each lane ends up owning 4 consecutive output columns of one row: 8/16-byte epilogue stores.
+#include <cstdio>
 #include <type_traits>
 #include <utility>
 
@@ -1239,7 +1240,8 @@ constexpr int S_RAW = S_RING;                  // raw LN partials of a tile's 25
 constexpr int S_LNROW = S_RAW + 256 * 8 * 8;   // merged (mean, rstd) per row (2 KiB)
 constexpr int S_COL = S_LNROW + 256 * 8;       // bias [256] | LN colsum [256] (2 KiB)
 constexpr int S_STAT = S_COL + 2 * 256 * 4;    // residual epilogue: per (row, column wave) sum / M2 (8 KiB)
-constexpr int S_SMEM = S_STAT + 256 * 4 * 8;   // 156 KiB
+constexpr int S_FLAG = S_STAT + 256 * 4 * 8;   // stream-K: the polled hand-off result, broadcast to the waves (16 B)
+constexpr int S_SMEM = S_FLAG + 16;             // 156 KiB + 16 B
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt_n() {   // s_waitcnt vmcnt(N), N < 64
@@ -1316,6 +1318,15 @@ __device__ __forceinline__ void lds_wr64(void* p, float2 v) {
   const f32x2 w = f32x2{v.x, v.y};
   asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(p)), "v"(w) : "memory");
 }
+// stream-K diagnostics (pdm_set_gemm_tuning bit 8): tails run, hand-offs not taken, summed poll time
+__device__ unsigned long long g_sk_stats[4];
+
+// a copy of x the compiler cannot see through: values derived from it are computed where they are used instead of
+// being hoisted and held in registers across loops
+__device__ __forceinline__ int opaque_i(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 __device__ __forceinline__ void lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -1369,10 +1380,29 @@ __device__ __forceinline__ TV tile_view(const GemmArgs& p, const TV& t2, bool se
 
 // GRP = 1: the grouped kernel (a second problem p2 from tile nt0 on, gemm8g_kernel); GRP = 0 compiles the one-problem
 // kernel with every view resolved to p at compile time
-template <int EPI, int MXO, int GRP>
+//
+// SK = 1: stream-K (one problem).  A partly filled last wave of tiles (the U-ViT's N = 1024 Linears at 100 rows:
+// 404 tiles on 256 CUs = a makespan of 2 tiles for 1.58 tiles of work) is removed by giving every workgroup an equal
+// share of the group's K-steps instead of whole tiles.  Workgroup j of an XCD group owns the K-step range
+// [B(j), B(j+1)) of the group's tile order (tile-major, 64-deep K-steps; boundaries on even K-steps), i.e. the tail
+// (K-steps s..nk) of a tile T0 whose head (0..s) the group's workgroup j-1 owns, whole tiles, and the head of a tile
+// T1 whose tail workgroup j+1 owns.  It runs them in the order head, whole tiles, tail:
+//  * head: the K-steps 0..s of T1 run as usual, then the fp32 accumulators go to this workgroup's slab (write-through
+//    sc1 stores, overlapped with the next segment's first K-steps like an epilogue's stores) and a flag is raised
+//    once every wave's stores have retired (one lane, relaxed agent-scope store behind a workgroup barrier);
+//  * tail: every wave drains, one lane polls the predecessor's flag (sc1 loads, bounded by 20 us), the waves load its
+//    slab straight into the accumulators (sc1 loads) and CONTINUE the MFMA chain from K-step s -- the same sequence
+//    of accumulations as one workgroup running the whole tile, so the result is bit-identical to SK = 0 and to the
+//    batch-size-independent tile arithmetic the sampler relies on.  Should the flag not come (the producer not yet
+//    resident, e.g. beside another lane's kernel), the tail is recomputed from K-step 0 instead: no workgroup ever
+//    waits unboundedly on another, and both branches give the same bits.
+// The producer's head runs first and needs nothing, so the flag is normally up long before the consumer's tail
+// (margin = share - nk K-steps); gemm_launch takes SK only where every workgroup's share is >= nk + 4 K-steps.
+template <int EPI, int MXO, int GRP, int SK = 0>
 __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int ntiles, const TV& p2, int nt0) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_RES, "persistent kernel epilogues");
   static_assert(!MXO || EPI != EPI_RES, "MXFP8 output: bf16 / GELU epilogues");
+  static_assert(!SK || !GRP, "stream-K: one problem");
   constexpr int ROWB = 128;
   constexpr int HALF = 128 * ROWB;
   constexpr int BUF = 4 * HALF;
@@ -1393,10 +1423,54 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
   const int tstart = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
   const int tcnt = q8 + (x < r8 ? 1 : 0);
   const int nx = (G >> 3) + (x < (G & 7) ? 1 : 0);
-  const int ntl = tcnt > jw ? (tcnt - jw + nx - 1) / nx : 0;
+  const int nk = p.K / 64;   // >= 4 (gemm_launch)
+  // segments: SK = 0 the tiles tstart + jw + i * nx (whole); SK = 1 [head of tile ht] [whole tiles tf0 ..] [tail]
+  int ntl;
+  int ht = 0, hke = 0, tf0 = 0, nf = 0, tt = 0, tkb = 0;
+  bool has_head = false, has_tail = false;
+  if constexpr (SK) {
+    const long long I = (long long)tcnt * nk;
+    auto bnd = [&](int j) {   // boundary j of the group's K-step range, on an even K-step, no piece shorter than 2
+      const long long b = I * j / nx;
+      int t = (int)(b / nk), o = (int)(b - (long long)t * nk);
+      o &= ~1;
+      if (nk - o < 2) {
+        o = 0;
+        ++t;
+      }
+      return t * nk + o;
+    };
+    const int sa = bnd(jw), sb = bnd(jw + 1);
+    const int ta = sa / nk, oa = sa - ta * nk, tb = sb / nk, ob = sb - tb * nk;
+    has_tail = oa > 0;
+    tt = ta;
+    tkb = oa;
+    tf0 = has_tail ? ta + 1 : ta;
+    nf = tb - tf0;
+    has_head = ob > 0;
+    ht = tb;
+    hke = ob;
+    ntl = (has_head ? 1 : 0) + nf + (has_tail ? 1 : 0);
+  } else {
+    ntl = tcnt > jw ? (tcnt - jw + nx - 1) / nx : 0;
+  }
   if (ntl == 0) return;
-  auto tile_mn = [&](int i, int& m0_, int& n0_, bool& second) {
-    int u = tstart + jw + i * nx;
+  // segment i: group-global tile u, K-steps [kb, ke), kind 0 whole / 1 head (-> slab) / 2 tail (<- slab)
+  auto seg = [&](int i, int& u, int& kb_, int& ke_, int& kd) {
+    if constexpr (SK) {
+      const int j = i - (has_head ? 1 : 0);
+      if (has_head && i == 0) {
+        u = tstart + ht; kb_ = 0; ke_ = hke; kd = 1;
+      } else if (j < nf) {
+        u = tstart + tf0 + j; kb_ = 0; ke_ = nk; kd = 0;
+      } else {
+        u = tstart + tt; kb_ = tkb; ke_ = nk; kd = 2;
+      }
+    } else {
+      u = tstart + jw + i * nx; kb_ = 0; ke_ = nk; kd = 0;
+    }
+  };
+  auto tile_mn = [&](int u, int& m0_, int& n0_, bool& second) {
     second = GRP && u >= nt0;
     if (second) u -= nt0;
     const int tiles_m = ((GRP && second ? p2.M : p.M) + BM2 - 1) / BM2;
@@ -1517,52 +1591,124 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
     __builtin_amdgcn_s_setprio(0);
   };
 
-  const int nk = p.K / 64;   // >= 4 (gemm_launch)
   int m0, n0;
   bool sec;
-  tile_mn(0, m0, n0, sec);
+  int u0, kb, ke, kind;
+  seg(0, u0, kb, ke, kind);
+  tile_mn(u0, m0, n0, sec);
   TV cv = tile_view(p, p2, GRP && sec), nv = cv;
   set_tile(cv, m0, n0);
   set_out(cv);   // one problem: the output descriptors are built once (grouped: again per tile)
-  // prologue of the first tile: tables, K-tile 0, A0 W0 W1 of K-tile 1; the wait retires the tables and A0 W0 W1(0)
+  // prologue of the first segment: tables, K-tile kb, A0 W0 W1 of K-tile kb+1; the wait retires the tables and
+  // A0 W0 W1(kb)
   issue_tables(cv, m0, n0);
-  issue(0, 0, KA0);
-  issue(0, 0, KW0);
-  issue(0, 0, KW1);
-  issue(0, 0, KA1);
-  issue(1, 1, KA0);
-  issue(1, 1, KW0);
-  issue(1, 1, KW1);
+  issue(0, kb, KA0);
+  issue(0, kb, KW0);
+  issue(0, kb, KW1);
+  issue(0, kb, KA1);
+  issue(1, kb + 1, KA0);
+  issue(1, kb + 1, KW0);
+  issue(1, kb + 1, KW1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   bar_raw();
 
+  int g = 0;                  // K-steps run so far: the ring slot of the next one is g & 1
+  bool pub_pending = false;   // SK: this workgroup's head slab stored, its flag not yet raised
+  auto publish = [&]() {
+    if (tid == 0) __hip_atomic_store(p.sk_flags + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pub_pending = false;
+  };
   for (int it = 0; it < ntl; ++it) {
     const bool has_next = it + 1 < ntl;
-    int m0n = 0, n0n = 0;
+    int m0n = 0, n0n = 0, kbn = 0, ken = 0, kindn = 0;
     if (has_next) {
       bool secn;
-      tile_mn(it + 1, m0n, n0n, secn);
+      int un;
+      seg(it + 1, un, kbn, ken, kindn);
+      tile_mn(un, m0n, n0n, secn);
       if constexpr (GRP) nv = tile_view(p, p2, secn);   // one problem: nv == cv throughout
     }
 #pragma unroll
     for (int f = 0; f < 32; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int par = (it * nk) & 1;   // ring slot of the tile's K-tile 0
+    // the previous segment's epilogue stores (E per lane; a head's slab: 32) are younger than the ring loads the
+    // first K-tile waits for
+    bool after_epi = it > 0;
+    const bool after_slab = SK && it == 1 && has_head;
+    if constexpr (SK) {
+      if (kind == 2) {
+        // tail: every wave drains (ring prefetch of this tile, the previous epilogue's / slab's stores), so the own
+        // head's flag can go up now; then take over the predecessor's accumulators
+        wait_vmcnt_n<0>();
+        bar_raw();
+        if (pub_pending) publish();
+        if (tid == 0) {
+          const unsigned* fl = p.sk_flags + blockIdx.x - 8;
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          unsigned ok = 0;
+          for (; !(p.dbg_tile0 & 128);) {   // dbg bit 7 (tests): never take the hand-off, recompute the tile
+            if (__hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+              ok = 1;
+              break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 2000ull) break;   // 20 us (100 MHz)
+            __builtin_amdgcn_s_sleep(2);
+          }
+          if (p.dbg_tile0 & 256) {   // diagnostics: tails, hand-offs not taken, poll time (10 ns ticks)
+            atomicAdd(&g_sk_stats[0], 1ull);
+            if (!ok) atomicAdd(&g_sk_stats[1], 1ull);
+            atomicAdd(&g_sk_stats[2], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
+          }
+          asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(lds_addr(smem + S_FLAG)), "v"(ok) : "memory");
+        }
+        bar_raw();
+        unsigned okv;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(okv) : "v"(lds_addr(smem + S_FLAG)) : "memory");
+        if (p.dbg_tile0 & 512) {   // timing experiment: the hand-off without its slab traffic (wrong results)
+        } else if (__builtin_amdgcn_readfirstlane(okv)) {
+          // sc1 loads (L1 bypassed) of the sc1-stored slab, behind the polling wave's match + the barrier
+          const __amdgpu_buffer_rsrc_t rsl = make_rsrc(p.sk_slab + (size_t)(blockIdx.x - 8) * 65536, 262144);
+#pragma unroll
+          for (int f = 0; f < 32; ++f) {
+            const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsl, opaque_i(tid) * 16, f * 8192, 16);
+            acc[f] = __builtin_bit_cast(f32x4, v);
+          }
+          // consume them here: the compiler's own waits for these loads then sit in this branch, not in front of
+          // every segment's first MFMAs (its wait tracking merges the branches)
+#pragma unroll
+          for (int f = 0; f < 32; ++f) asm volatile("" : "+v"(acc[f]));
+        } else {
+          // no hand-off: the whole tile here.  The ring's K-tiles kb, kb+1 have landed (drained above) and nobody
+          // reads them: re-prime the same slots with K-tiles 0, 1 as the kernel prologue does
+          kb = 0;
+          issue(g & 1, 0, KA0);
+          issue(g & 1, 0, KW0);
+          issue(g & 1, 0, KW1);
+          issue(g & 1, 0, KA1);
+          issue((g + 1) & 1, 1, KA0);
+          issue((g + 1) & 1, 1, KW0);
+          issue((g + 1) & 1, 1, KW1);
+          wait_vmcnt_n<8>();
+          bar_raw();
+        }
+        after_epi = false;
+      }
+    }
     if (wave >= 4) bar_raw();        // stagger: waves 4-7 one barrier behind
-    for (int kt = 0; kt < nk; ++kt) {
-      const int slot = (par + kt) & 1;
+    for (int kt = kb; kt < ke; ++kt, ++g) {
+      const int slot = g & 1;
       const char* buf = smem + slot * BUF;
-      // the previous tile's epilogue stores (E per lane) are younger than the ring loads this K-tile waits for
-      const bool after_epi = kt == 0 && it > 0;
-      const bool m1 = kt + 1 < nk || has_next;   // K-tile g+1 exists (this tile's kt+1 or the next tile's 0)
-      const bool m2 = kt + 2 < nk || has_next;   // K-tile g+2 (nk >= 4: the next tile's kt+2-nk <= 1)
+      const bool first = kt == kb && after_epi;
+      const bool m1 = kt + 1 < ke || has_next;   // K-tile g+1 exists (this segment's kt+1 or the next one's kbn)
+      const bool m2 = kt + 2 < ke || has_next;   // K-tile g+2 (segments >= 2 K-tiles: the next one's kbn + {0, 1})
       // phase A: quadrants (0,0) (0,1); issues A1 of K-tile g+1
       read_a(buf, 0);
       read_w(buf, 0);
       read_w(buf, 1);
       lds_done();
       if (m1) {
-        issue(slot ^ 1, kt + 1 < nk ? kt + 1 : 0, KA1);
-        if (after_epi) wait_vmcnt_n<8 + E>();
+        issue(slot ^ 1, kt + 1 < ke ? kt + 1 : kbn, KA1);
+        if (first && after_slab) wait_vmcnt_n<8 + 32>();
+        else if (first) wait_vmcnt_n<8 + E>();
         else wait_vmcnt_n<8>();
       } else {
         wait_vmcnt_n<0>();
@@ -1571,26 +1717,50 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       mma(0, 0);
       mma(0, 1);
       bar_raw();
-      // phase B: quadrants (1,0) (1,1); issues A0 W0 W1 of K-tile g+2 (the next tile's from kt = nk-2 on)
+      // phase B: quadrants (1,0) (1,1); issues A0 W0 W1 of K-tile g+2 (the next segment's from kt = ke-2 on)
       read_a(buf, 1);
       lds_done();
-      if (kt == nk - 2 && has_next) set_tile(nv, m0n, n0n);
+      if (kt == ke - 2 && has_next) set_tile(nv, m0n, n0n);
       if (m2) {
-        const int k2 = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
+        const int k2 = kt + 2 < ke ? kt + 2 : kbn + (kt + 2 - ke);
         issue(slot, k2, KA0);
         issue(slot, k2, KW0);
         issue(slot, k2, KW1);
-        if (after_epi) wait_vmcnt_n<8 + E>();
+        if (first && after_slab) wait_vmcnt_n<8 + 32>();
+        else if (first) wait_vmcnt_n<8 + E>();
         else wait_vmcnt_n<8>();
       } else if (m1) {
         wait_vmcnt_n<2>();
       }
       bar_raw();
+      // SK: the head slab's stores are older than everything this K-tile's phase-A wait left in flight, and by this
+      // barrier every wave (4-7 one barrier behind) has passed that wait: raise the flag
+      if constexpr (SK) {
+        if (pub_pending && kt == kb + 1) publish();
+      }
       mma(1, 0);
       mma(1, 1);
       bar_raw();
     }
     if (wave < 4) bar_raw();   // rejoin the stagger
+
+    if constexpr (SK) {
+      if (kind == 1) {   // head: accumulators -> slab (sc1 write-through), the next tile's tables
+        if (has_next) issue_tables(nv, m0n, n0n);
+        const __amdgpu_buffer_rsrc_t rsl = make_rsrc(p.sk_slab + (size_t)blockIdx.x * 65536, 262144);
+#pragma unroll
+        for (int f = 0; f < 32; ++f)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[f]), rsl,
+                                                 (p.dbg_tile0 & 512) ? (int)OOB : opaque_i(tid) * 16, f * 8192, 16);
+        pub_pending = true;
+        m0 = m0n;
+        n0 = n0n;
+        kb = kbn;
+        ke = ken;
+        kind = kindn;
+        continue;
+      }
+    }
 
     if (p.dbg_tile0 & 16) {    // timing experiment: no epilogue (its E stores still issued, to nowhere)
 #pragma unroll
@@ -1601,6 +1771,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       for (int s = 0; s < E; ++s) __builtin_amdgcn_raw_buffer_store_b32(0, rout, (int)OOB, 0, 0);
       m0 = m0n;
       n0 = n0n;
+      kb = kbn;
+      ke = ken;
+      kind = kindn;
       if constexpr (GRP) cv = nv;
       continue;
     }
@@ -1610,11 +1783,14 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
     const int M = cv.M;
     // this lane's columns: fragment (qj, ni) covers n0 + qj*128 + wn*32 + ni*16 + g4*4 + [0, 4)
     f32x4 bv[2][2], cs[2][2];
-    lds_rd_cols(smem + S_COL + (wn * 32 + g4 * 4) * 4, bv, cs);
+    // lane-derived LDS addresses recomputed here from an opaque copy of tid, not held across the K-loop (the
+    // residual epilogue runs at the 256-VGPR limit)
+    const int tid_e = opaque_i(tid), g4e = (tid_e & 63) >> 4, r16e = tid_e & 15;
+    lds_rd_cols(smem + S_COL + (wn * 32 + g4e * 4) * 4, bv, cs);
     char* lnrow = smem + S_LNROW;
     if (ln && tid < 256) {
       f32x2 raw[8];
-      lds_rd_raw(smem + S_RAW + tid * p.ln_ld * 8, raw);
+      lds_rd_raw(smem + S_RAW + tid_e * p.ln_ld * 8, raw);
       float2 lst[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) lst[t] = t < p.ln_ld ? make_float2(raw[t][0], raw[t][1]) : make_float2(0.f, 0.f);
@@ -1634,7 +1810,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
     float2 mrow[2][4];   // (mean, rstd) of the lane's 8 rows
     {
       f32x2 mr8[8];
-      lds_rd_rows(lnrow + (wm * 64 + r16) * 8, mr8);
+      lds_rd_rows(lnrow + (wm * 64 + r16e) * 8, mr8);
 #pragma unroll
       for (int qi = 0; qi < 2; ++qi)
 #pragma unroll
@@ -1808,7 +1984,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       lds_sync();
       bar_raw();
       {   // one float per thread: row tid >> 1, component tid & 1 (sum, M2)
-        const int ml = tid >> 1, c = tid & 1;
+        const int tid_s = opaque_i(tid), ml = tid_s >> 1, c = tid_s & 1;
         f32x2 t4[4];
         lds_rd_stat2(tab + ml * 32, t4);
         const float S = (t4[0][0] + t4[1][0]) + (t4[2][0] + t4[3][0]);
@@ -1830,15 +2006,18 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
     }
     m0 = m0n;
     n0 = n0n;
+    kb = kbn;
+    ke = ken;
+    kind = kindn;
     if constexpr (GRP) cv = nv;
   }
 }
 
 // the one-problem kernel keeps its own signature (a second by-value GemmArgs in every launch measured +0.7 % on the
 // L/2 forward); the grouped kernel takes both problems
-template <int EPI, int MXO = 0>
+template <int EPI, int MXO = 0, int SK = 0>
 __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n, int ntiles) {
-  gemm8s_body<EPI, MXO, 0>(p, tiles_n, ntiles, TV{}, ntiles);
+  gemm8s_body<EPI, MXO, 0, SK>(p, tiles_n, ntiles, TV{}, ntiles);
 }
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm8g_kernel(GemmArgs p, int tiles_n, int ntiles, TV p2, int nt0) {
@@ -2411,6 +2590,17 @@ const char* gemm_check(const GemmArgs& p, int epi) {
 }
 
 static int g_gemm_algo = 0;
+static int g_gemm_sk = 0;   // off by default: measured slower at every U-ViT shape (profiles/r05a, r05b)
+static long long g_sk_launches = 0;   // stream-K launches so far (host count, tests)
+void gemm_set_sk(int mode) { g_gemm_sk = mode; }
+int gemm_get_sk() { return g_gemm_sk; }
+long long gemm_sk_launches() { return g_sk_launches; }
+int gemm_sk_stats(unsigned long long* out) {   // reads and clears the device counters (synchronises the device)
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sk_stats), 3 * sizeof(unsigned long long)) != hipSuccess) return 1;
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sk_stats), z, sizeof(z)) != hipSuccess;
+}
 void gemm_set_tuning(int raster, int dbg_tile0) { g_gemm_raster = raster; g_gemm_dbg = dbg_tile0; }  // 0 auto, 1 = 128x128, 2 = 256x256 BK32 x4 ring, 3 = 256x256 BK64 x2, 4 = 256x256 8-phase
 void gemm_set_algo(int algo) { g_gemm_algo = algo; }
 
@@ -2540,6 +2730,41 @@ static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream, const
   const int ntiles = nt0 + (p2 ? (p2->M + BM2 - 1) / BM2 * tn : 0);
   const GemmArgs& q = p2 ? *p2 : p;
   const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
+  // stream-K where the last wave of tiles leaves CUs idle and every workgroup's share is >= nk + 4 K-steps (so each
+  // tile has at most two pieces and the consumer's tail normally finds its flag up, gemm8s_body)
+  bool sk = false;
+  if (!p2 && p.sk_flags && p.sk_slab && g_gemm_sk && ntiles > grid && grid <= SK_FLAG_WORDS && grid >= 8 &&
+      ntiles % grid) {
+    const int nk = p.K / 64, gx = (grid + 7) / 8, tmin = ntiles / 8;
+    const int waves = (ntiles + grid - 1) / grid;
+    const double fill = (double)ntiles / ((double)waves * grid);
+    sk = (long long)tmin * nk >= (long long)gx * (nk + 4) && (g_gemm_sk == 2 || fill < 0.97);
+  }
+  if (sk) {
+    ++g_sk_launches;
+    static bool attr_sk = false;
+    if (!attr_sk) {
+      (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_GELU, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_RES, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_GELU, 1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      attr_sk = true;
+    }
+    if (p.out_fp8) {
+      if (epi == EPI_BF16) hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 1, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+      else if (epi == EPI_GELU) hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 1, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+      else return hipErrorInvalidValue;
+      return hipGetLastError();
+    }
+    switch (epi) {
+      case EPI_BF16: hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 0, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
+      case EPI_GELU: hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 0, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
+      case EPI_RES: hipLaunchKernelGGL((gemm8s_kernel<EPI_RES, 0, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (p.out_fp8) {   // fits_8s: bf16 / GELU with the MXFP8 copy as the only output
     if (epi == EPI_BF16) hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
     else if (epi == EPI_GELU) hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
@@ -2574,8 +2799,33 @@ static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream, const
 // the persistent kernel's preconditions (epilogues, no conv / batch / gather / MXFP8 operands, K >= 256, one A
 // stride, buffer extents); an MXFP8 output only as the sole output of a bf16 / GELU epilogue (gemm_check has
 // validated its shape: N % 32, ldo8 % 16, out_scale_ld >= M)
+// The persistent kernel counts its VMEM ops by hand (the ring's vmcnt waits): a register spill would add scratch
+// traffic it does not expect, so every instantiation is checked once for a private segment; with one, the
+// persistent policy is off (whole-tile algo 7 instead) and the library says so on stderr.
+static bool persist_kernels_ok() {
+  static int ok = -1;
+  if (ok < 0) {
+    const void* fns[] = {(const void*)gemm8s_kernel<EPI_BF16>, (const void*)gemm8s_kernel<EPI_GELU>,
+                         (const void*)gemm8s_kernel<EPI_RES>, (const void*)gemm8s_kernel<EPI_BF16, 1>,
+                         (const void*)gemm8s_kernel<EPI_GELU, 1>, (const void*)gemm8s_kernel<EPI_BF16, 0, 1>,
+                         (const void*)gemm8s_kernel<EPI_GELU, 0, 1>, (const void*)gemm8s_kernel<EPI_RES, 0, 1>,
+                         (const void*)gemm8s_kernel<EPI_BF16, 1, 1>, (const void*)gemm8s_kernel<EPI_GELU, 1, 1>,
+                         (const void*)gemm8g_kernel<EPI_BF16>, (const void*)gemm8g_kernel<EPI_GELU>,
+                         (const void*)gemm8g_kernel<EPI_RES>};
+    ok = 1;
+    for (const void* f : fns) {
+      hipFuncAttributes at{};
+      if (hipFuncGetAttributes(&at, f) != hipSuccess) continue;   // no device: the launch itself will fail
+      if (at.localSizeBytes > 0) ok = 0;
+    }
+    if (!ok) fprintf(stderr, "libpdm: a persistent GEMM instantiation uses scratch (register spill); using algo 7\n");
+  }
+  return ok == 1;
+}
+
 static bool fits_8s(const GemmArgs& p, int epi) {
   const long long lim = 0x7fffffffLL;
+  if (!persist_kernels_ok()) return false;
   if (epi != EPI_BF16 && epi != EPI_GELU && epi != EPI_RES) return false;
   if (p.conv || p.batch > 1 || p.a_rows_per_group > 0 || p.fp8 || p.mx_center) return false;
   if (p.out_fp8) {
@@ -2645,8 +2895,11 @@ hipError_t gemm_launch_pair(const GemmArgs& a, const GemmArgs& b, int epi, hipSt
   // arithmetic -- and the sampler's batch invariance -- does not depend on the other problem's rows
   if (algo_ok && same && p.M >= 4096 && q.M >= 4096 && p.N >= 256 && fits_8s(p, epi) && fits_8s(q, epi))
     return launch8s(p, epi, stream, &q);
-  const hipError_t e = gemm_launch(a, epi, stream);
-  return e != hipSuccess ? e : gemm_launch(b, epi, stream);
+  GemmArgs a1 = a, b1 = b;   // one flag block serves one launch
+  a1.sk_flags = b1.sk_flags = nullptr;
+  a1.sk_slab = b1.sk_slab = nullptr;
+  const hipError_t e = gemm_launch(a1, epi, stream);
+  return e != hipSuccess ? e : gemm_launch(b1, epi, stream);
 }
 
 hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
@@ -2693,6 +2946,8 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
     const int m1 = p.conv ? (p.M / hw / 2) * hw : ((p.M / 2 + BM2 - 1) / BM2) * BM2;
     if (m1 > 0 && m1 < p.M) {
       GemmArgs a = args, b = args;
+      a.sk_flags = b.sk_flags = nullptr;   // one flag block serves one launch
+      a.sk_slab = b.sk_slab = nullptr;
       a.M = m1;
       b.M = p.M - m1;
       if (p.conv) b.A1 += (size_t)(m1 / hw) * (p.convH >> p.conv_up) * (p.convW >> p.conv_up) * p.convC;

@@ -77,8 +77,20 @@ struct GemmArgs {
   // EPI_GELU activation: 0 = exact-erf GELU (nn.GELU, libs/timm.py:102), 1 = quick GELU x * sigmoid(1.702 x)
   // (the CLIP text encoder's hidden_act, transformers CLIPMLP)
   int act;
+  // stream-K state of the persistent kernel (gemm.hip gemm8s_body SK = 1), both or neither: sk_flags >= 256 zeroed
+  // words owned by THIS launch (one per workgroup: "head slab published"), sk_slab >= 256 x 64 Ki floats (one fp32
+  // 256 x 256 accumulator tile per workgroup).  Null: whole tiles only.
+  unsigned* sk_flags;
+  float* sk_slab;
 };
 void gemm_set_tuning(int raster, int dbg_tile0);
+// stream-K policy: 0 off (default), 1 auto (where the last wave of tiles is < 97 % full), 2 wherever it applies
+void gemm_set_sk(int mode);
+int gemm_get_sk();
+long long gemm_sk_launches();
+int gemm_sk_stats(unsigned long long* out3);
+constexpr int SK_FLAG_WORDS = 256;                       // flags per launch
+constexpr long long SK_SLAB_BYTES = 256LL * 65536 * 4;   // 64 MiB
 
 // Row partials of the fused LayerNorm: X fp32 [rows, D] -> stats [rows, ceil(D/256)] (sum, M2) per 256-column
 // group (+ optional bf16 copy xb [rows, D], + optional MXFP8 copy xq / xs in the GemmArgs A-operand layout).  Used where no GEMM epilogue produced them (token assembly, the

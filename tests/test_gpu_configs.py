@@ -69,6 +69,32 @@ def test_full_t2i_forward_with_mask_vs_oracle(dev, coco):
     assert rel(pm, ref_pm) < 2e-2
 
 
+def test_full_t2i_forward_grouped_rows_vs_oracle(dev, coco):
+    """At >= 13 rows every image- / mask-stream Linear pair of a layer is ONE grouped persistent launch (capi.hip
+    run_block16_pair -> pdm::gemm_launch_pair: both problems >= 4096 rows); the B <= 3 tests above take its two-launch
+    fallback.  The grouped forward at B = 14 against the fp32 oracle (2e-2, as above) and against the same forward
+    with grouping off (pdm_set_gemm_algo(7): separate whole-tile launches) to bf16 rounding (1e-2)."""
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    from panopticdiffusionmodels_amd import _lib
+    net, sd, cfg = coco
+    kw = dict(cfg)
+    kw.pop("name")
+    x, t, ctx, mt = _t2i_inputs(14, seed=3)
+    with torch.no_grad():
+        eps, pm = net(x.to(dev), t.to(dev), ctx.to(dev), mask_token=mt.to(dev))
+        _lib.check(_lib.load().pdm_set_gemm_algo(7), "pdm_set_gemm_algo")
+        try:
+            eps7, pm7 = net(x.to(dev), t.to(dev), ctx.to(dev), mask_token=mt.to(dev))
+        finally:
+            _lib.load().pdm_set_gemm_algo(0)
+        ref_eps, ref_pm = uvit_ref.uvit_t2i_forward(sd, kw, x, t, ctx, mask_token=mt)
+    assert torch.isfinite(eps).all() and torch.isfinite(pm).all()
+    assert rel(eps, ref_eps) < 2e-2
+    assert rel(pm, ref_pm) < 2e-2
+    assert rel(eps, eps7) < 1e-2
+    assert rel(pm, pm7) < 1e-2
+
+
 def test_full_t2i_forward_no_mask_and_ground_truth_vs_oracle(dev, coco):
     net, sd, cfg = coco
     kw = dict(cfg)

@@ -494,18 +494,21 @@ def test_lincomb(lib):
     assert rel(out, ts[0] - 0.5 * ts[1] + 0.25 * ts[2] + 3 * ts[3]) < 1e-6
 
 
-@pytest.mark.parametrize("case", ["qkv_ln", "fc1_ln_gelu", "proj_res", "fc2_res", "skip_split", "mixed_n"])
+@pytest.mark.parametrize("case", ["qkv_ln", "fc1_ln_gelu", "proj_res", "fc2_res", "fc2_res_inplace", "skip_split",
+                                  "mixed_n"])
 def test_gemm_pair_grouped_vs_separate(lib, case):
     """pdm_gemm_pair (one grouped persistent launch over the t2i image- and mask-stream Linears of a layer, csrc
     capi.hip run_block16_pair) against the same two GEMMs launched alone: bit-identical outputs and partials (each
     tile runs the same arithmetic in either launch).  Rows of the two problems as at the t2i bench (32 rows x 334 /
-    590 tokens), D = 512; 'mixed_n' cannot be grouped (different N) and takes the two-launch path."""
+    590 tokens), D = 512; 'mixed_n' cannot be grouped (different N) and takes the two-launch path.  The residual
+    cases accumulate res_in (as the forward's res_args); 'fc2_res_inplace' reads the residual from the output
+    itself (res_in == out, the image block's fc2 adding into XT2)."""
     D, Hd = 512, 2048
     Ma, Mb = 32 * 334, 32 * 590
     g = torch.Generator(device="cuda").manual_seed(hash(case) % 1000)
     N, K, epi = {"qkv_ln": (3 * D, D, lib.EPI_BF16), "fc1_ln_gelu": (Hd, D, lib.EPI_GELU), "proj_res": (D, D, lib.EPI_RES),
-                 "fc2_res": (D, Hd, lib.EPI_RES), "skip_split": (D, 2 * D, lib.EPI_RES),
-                 "mixed_n": (3 * D, D, lib.EPI_BF16)}[case]
+                 "fc2_res": (D, Hd, lib.EPI_RES), "fc2_res_inplace": (D, Hd, lib.EPI_RES),
+                 "skip_split": (D, 2 * D, lib.EPI_RES), "mixed_n": (3 * D, D, lib.EPI_BF16)}[case]
 
     def problem(M, n):
         kk = K // 2 if case == "skip_split" else K
@@ -516,7 +519,12 @@ def test_gemm_pair_grouped_vs_separate(lib, case):
         if case == "skip_split":
             kw["a2"] = torch.randn(M, kk, device="cuda", generator=g).bfloat16()
         if epi == lib.EPI_RES:
-            kw["res_in"] = torch.randn(M, n, device="cuda", generator=g).bfloat16()
+            if case == "fc2_res_inplace":
+                kw["out"] = torch.randn(M, n, device="cuda", generator=g).bfloat16()
+                kw["res_in"] = kw["out"]
+            else:
+                kw["res_in"] = torch.randn(M, n, device="cuda", generator=g).bfloat16()
+            kw["accumulate"] = True
             kw["stats_out"] = torch.empty(M, (n + 255) // 256, 2, device="cuda")
         else:
             _, st = lib.rowstats(torch.randn(M, K, device="cuda", generator=g) * 1.3 + 0.2, want_bf16=False)
@@ -525,12 +533,16 @@ def test_gemm_pair_grouped_vs_separate(lib, case):
 
     pa = problem(Mb, N)
     pb = problem(Ma, D if case == "mixed_n" else N)
+    init = [kw["out"].clone() for kw in (pa, pb)]
     ref = []
     for kw in (pa, pb):
         lib.gemm_ex(epi, **kw)
         ref.append({k: kw[k].clone() for k in ("out", "stats_out") if k in kw})
-    for kw in (pa, pb):
-        kw["out"].fill_(7.0)
+    for kw, o in zip((pa, pb), init):
+        if case == "fc2_res_inplace":
+            kw["out"].copy_(o)     # the residual it reads
+        else:
+            kw["out"].fill_(7.0)
         if "stats_out" in kw:
             kw["stats_out"].fill_(7.0)
     lib.gemm_pair(epi, pa, pb)
@@ -538,3 +550,9 @@ def test_gemm_pair_grouped_vs_separate(lib, case):
     for kw, r in zip((pa, pb), ref):
         for k, v in r.items():
             assert torch.equal(kw[k], v), (case, k)
+    if epi == lib.EPI_RES:   # the residual really entered the sum (fp32 torch on the same bf16 operands)
+        for kw, o in zip((pa, pb), init):
+            a = torch.cat([kw["a"], kw["a2"]], 1) if "a2" in kw else kw["a"]
+            res = o if case == "fc2_res_inplace" else kw["res_in"]
+            want = a.float() @ kw["w"].float().t() + kw["bias"] + res.float()
+            assert rel(kw["out"].float(), want) < 1e-2, case
