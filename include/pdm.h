@@ -47,7 +47,9 @@ int pdm_device_arch(char* buf, int len);
  *         bf16-residual epilogues, K >= 256: the automatic choice where it applies, else 7)
  *   attention: 1 = streamed K/V per 64-query block, 2 / 3 = head-resident K/V with 2 / 3 query tiles per wave,
  *              4 = head-resident v2 (Dh 64), 7 = head-resident Dh 72 (64 + 8 split); 5/6, 8/9 = their load-only /
- *              math-only timing variants (wrong results) */
+ *              math-only timing variants (wrong results); 11 = persistent head-resident Dh 64 with the next head's
+ *              K/V streamed in during the last pass (12 / 13 its load-only / math-only timing variants); 14 = the
+ *              same for Dh 72 (15 / 16 timing variants) */
 /* GEMM tile-order knob: raster = row panels per tile group inside an XCD's tile range (0 = row-major);
  * dbg_tile0 bit 0 stages every tile's operands from tile (0, 0); bit 1 lets a bf16 GEMM run with no output (mainloop +
  * LDS staging only); bit 4 skips every 256-tile epilogue -- timing experiments, results are wrong; bit 7 (tests):

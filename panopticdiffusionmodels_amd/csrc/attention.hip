@@ -24,6 +24,58 @@ __device__ __forceinline__ s16x4 lds_read_tr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((PDM_LDS s16x4*)(p));
 }
 
+// K / V staging of the head-resident kernels: 16-byte LDS-DMA through a buffer descriptor (the rows of one batch
+// entry), not the global-address form -- after a global_load_lds hipcc drains vmcnt to 0 before the next LDS read
+// (it cannot tell the DMA's destination from the block being read), which serialised every head's first pass behind
+// its whole K/V transfer; the buffer form leaves the ordering to the kernels' own counted waits
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t att_rsrc(const void* base, long long bytes) {
+  const unsigned n = bytes >= 0x7fffffffLL ? 0x7fffffffu : (unsigned)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)n, 0x00020000);
+}
+__device__ __forceinline__ void att_dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, PDM_LDS void* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds, 16, (int)voff, 0, 0, 0);
+}
+
+// V^T fragment reads of one 32-key step as ONE asm statement with its lgkmcnt wait: hipcc treats the transposed-read
+// builtin as aliasing any pending LDS-DMA and waits vmcnt(0) in front of it (draining the K/V transfer still in
+// flight); the data read here were retired by the kernels' counted vmcnt waits + barriers.
+__device__ __forceinline__ unsigned att_lds_addr(const void* p) { return (unsigned)(uintptr_t)(PDM_LDS const void*)p; }
+__device__ __forceinline__ bf16x8 att_pair(s16x4 lo, s16x4 hi) {
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+// Dh 64: four fragments, fragment dt = rows at a[dt] and a[dt] + 2048
+__device__ __forceinline__ void lds_vt4(const char* a0, const char* a1, const char* a2, const char* a3, bf16x8 (&vf)[4]) {
+  s16x4 l0, h0, l1, h1, l2, h2, l3, h3;
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %8\n\tds_read_b64_tr_b16 %1, %8 offset:2048\n\t"
+      "ds_read_b64_tr_b16 %2, %9\n\tds_read_b64_tr_b16 %3, %9 offset:2048\n\t"
+      "ds_read_b64_tr_b16 %4, %10\n\tds_read_b64_tr_b16 %5, %10 offset:2048\n\t"
+      "ds_read_b64_tr_b16 %6, %11\n\tds_read_b64_tr_b16 %7, %11 offset:2048\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(l0), "=&v"(h0), "=&v"(l1), "=&v"(h1), "=&v"(l2), "=&v"(h2), "=&v"(l3), "=&v"(h3)
+      : "v"(att_lds_addr(a0)), "v"(att_lds_addr(a1)), "v"(att_lds_addr(a2)), "v"(att_lds_addr(a3))
+      : "memory");
+  vf[0] = att_pair(l0, h0);
+  vf[1] = att_pair(l1, h1);
+  vf[2] = att_pair(l2, h2);
+  vf[3] = att_pair(l3, h3);
+}
+// Dh 72 (144-B rows): five fragments, fragment dt = rows at a + 32 dt and a + 2304 + 32 dt
+__device__ __forceinline__ void lds_vt5(const char* a, bf16x8 (&vf)[5]) {
+  s16x4 l[5], h[5];
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %10\n\tds_read_b64_tr_b16 %1, %10 offset:2304\n\t"
+      "ds_read_b64_tr_b16 %2, %10 offset:32\n\tds_read_b64_tr_b16 %3, %10 offset:2336\n\t"
+      "ds_read_b64_tr_b16 %4, %10 offset:64\n\tds_read_b64_tr_b16 %5, %10 offset:2368\n\t"
+      "ds_read_b64_tr_b16 %6, %10 offset:96\n\tds_read_b64_tr_b16 %7, %10 offset:2400\n\t"
+      "ds_read_b64_tr_b16 %8, %10 offset:128\n\tds_read_b64_tr_b16 %9, %10 offset:2432\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(l[0]), "=&v"(h[0]), "=&v"(l[1]), "=&v"(h[1]), "=&v"(l[2]), "=&v"(h[2]), "=&v"(l[3]), "=&v"(h[3]),
+        "=&v"(l[4]), "=&v"(h[4])
+      : "v"(att_lds_addr(a))
+      : "memory");
+#pragma unroll
+  for (int dt = 0; dt < 5; ++dt) vf[dt] = att_pair(l[dt], h[dt]);
+}
+
 template <int DH>
 __global__ __launch_bounds__(256) void attention_kernel(AttentionArgs p, int nqt) {
   constexpr int KC = 64;
@@ -449,6 +501,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
   const int ngrp = Lp / 8;
   if (DEBUG != 2) {
     const int r8 = lane >> 3, pc = lane & 7;
+    const __amdgpu_buffer_rsrc_t rq = att_rsrc(p.qkv + (size_t)b * L * p.ldq, (long long)L * p.ldq * 2);
     for (int grp0 = 0; grp0 < ngrp; grp0 += 8) {
 #pragma unroll
       for (int i = 0; i < 8 / NW; ++i) {
@@ -456,11 +509,11 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
         if (grp < ngrp) {
           const int row = grp * 8 + r8;
           const int key = row < L ? row : L - 1;
-          const bf16* src = base + (size_t)key * p.ldq;
+          const unsigned rowoff = (unsigned)(key * p.ldq + h * DH);
           const int kc = pc ^ ((row >> 1) & 7);
           const int vc = ((((pc >> 1) ^ ((row >> 1) & 3)) << 1) | (pc & 1));
-          glds16(src + D + kc * 8, (PDM_LDS void*)(Ks + grp * 1024));
-          glds16(src + 2 * D + vc * 8, (PDM_LDS void*)(Vs + grp * 1024));
+          att_dma16(rq, (rowoff + D + kc * 8) * 2u, (PDM_LDS void*)(Ks + grp * 1024));
+          att_dma16(rq, (rowoff + 2 * D + vc * 8) * 2u, (PDM_LDS void*)(Vs + grp * 1024));
         }
       }
     }
@@ -577,15 +630,13 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
             pf[t][j] = (bf16)s[t][2 * kk][j];
             pf[t][4 + j] = (bf16)s[t][2 * kk + 1][j];
           }
+        bf16x8 vf[4];
+        lds_vt4(vbase[0] + c * 8192 + kk * 4096, vbase[1] + c * 8192 + kk * 4096, vbase[2] + c * 8192 + kk * 4096,
+                vbase[3] + c * 8192 + kk * 4096, vf);
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const char* v1 = vbase[dt] + c * 8192 + kk * 4096;
-          const s16x4 lo = lds_read_tr16(v1);
-          const s16x4 hi = lds_read_tr16(v1 + 2048);
-          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf, pf[t], acc[t][dt]);
-        }
+          for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf[dt], pf[t], acc[t][dt]);
         if constexpr (ONES) {
 #pragma unroll
           for (int t = 0; t < NT; ++t) acc[t][4] = mfma16x16x32(ones_row, pf[t], acc[t][4]);
@@ -651,6 +702,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
       for (int t = 0; t < 3; ++t)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) qf[t][ks] = *reinterpret_cast<const bf16x8*>(qptr(t < nt ? tl[t] : tl[0], ks));
+      // consumed here, so hipcc's waits for these loads stay in this branch (its wait tracking merges the branches:
+      // otherwise every MFMA / LDS read of the shared pass code waits vmcnt(0))
+      asm volatile("" : "+v"(qf[0][0]), "+v"(qf[0][1]), "+v"(qf[1][0]), "+v"(qf[1][1]), "+v"(qf[2][0]), "+v"(qf[2][1]));
     }
     if (!p.q_log2) {   // q not pre-scaled by the producer: scale * log2(e) applied here (one extra bf16 rounding)
 #pragma unroll
@@ -665,6 +719,258 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
+// Persistent head-resident attention (Dh = 64, round 5): attention_v2_kernel's math, but each workgroup loops over
+// heads bh = blockIdx, blockIdx + grid, ... and streams the NEXT head's K/V into LDS while its last pass over the
+// current head runs: after every 64-key block of that pass a barrier releases the block's LDS rows and the waves
+// issue the next head's rows for it.  v2 launches one workgroup per head, and every workgroup on the chip stages its
+// head at the same moment and then computes with the memory system idle (the phases stay in lockstep across the
+// chip); here K/V traffic runs beside the MFMA / exp work of the previous head.  Every wave runs the same number of
+// passes (1-3 tiles each, balanced), so the per-block barriers of the first head's first pass and of each releasing
+// last pass pair up across waves.  Needs nqt >= NW (every wave owns a tile).  DEBUG 1: loads only; 2: math only.
+template <int DEBUG, int NW>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v3_kernel(AttentionArgs p, int nqt, int Lp) {
+  constexpr int DH = 64;
+  constexpr int NA = 5;                  // four PV output tiles + the ones-row tile carrying the softmax row sums
+  constexpr float RESCALE_THR = 8.0f;    // deferred rescale (log2 units): P <= 2^8 in bf16, O / l stay fp32
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* Ks = lds;
+  char* Vs = lds + Lp * 128;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nbh = p.B * p.H, L = p.L, D = p.H * DH;
+  const int g = lane >> 4, col = lane & 15;
+  const int my_tiles = (nqt - wave + NW - 1) / NW;      // >= 1
+  const int npass = ((nqt + NW - 1) / NW + 2) / 3;      // uniform over the waves
+  const int ngrp = Lp / 8, nfull = L / 64, nch = (L + 63) / 64;
+  const int r8 = lane >> 3, pc = lane & 7;
+
+  // K / V row groups [grp0, grp1) of head (b, h) (8 rows x 128 B per group; wave w takes grp0 + w, + NW, ...)
+  auto stage = [&](int b_, int h_, int grp0, int grp1) {
+    if (DEBUG == 2) return;
+    const __amdgpu_buffer_rsrc_t rq = att_rsrc(p.qkv + (size_t)b_ * L * p.ldq, (long long)L * p.ldq * 2);
+    for (int grp = grp0 + wave; grp < grp1; grp += NW) {
+      const int row = grp * 8 + r8;
+      const int key = row < L ? row : L - 1;
+      const unsigned rowoff = (unsigned)(key * p.ldq + h_ * DH);
+      const int kc = pc ^ ((row >> 1) & 7);
+      const int vc = ((((pc >> 1) ^ ((row >> 1) & 3)) << 1) | (pc & 1));
+      att_dma16(rq, (rowoff + D + kc * 8) * 2u, (PDM_LDS void*)(Ks + grp * 1024));
+      att_dma16(rq, (rowoff + 2 * D + vc * 8) * 2u, (PDM_LDS void*)(Vs + grp * 1024));
+    }
+  };
+  // this wave's DMA ops of the first head past block c (the vmcnt that retires Q and blocks 0..c)
+  auto ops_after = [&](int c) {
+    int n = 0;
+    for (int grp = 8 * (c + 1) + ((wave - 8 * (c + 1)) % NW + NW) % NW; grp < ngrp; grp += NW) n += 2;
+    return n;
+  };
+  auto bar = []() {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  int bh = blockIdx.x;
+  int b = bh / p.H, h = bh - (bh / p.H) * p.H;
+  auto qptr = [&](int b_, int h_, int tile, int ks) {
+    int q = tile * 16 + col;
+    q = q < L ? q : L - 1;
+    return p.qkv + ((size_t)b_ * L + q) * p.ldq + h_ * DH + ks * 32 + g * 8;
+  };
+  // first head: Q of the first pass by inline asm ahead of the K/V DMA, then the whole head staged
+  const int nt0 = my_tiles / npass + (my_tiles % npass ? 1 : 0);
+  i32x4 q0[3][2];
+  if (DEBUG != 2) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) q0[t][ks] = gload16_asm(qptr(b, h, wave + NW * min(t, nt0 - 1), ks));
+  }
+  stage(b, h, 0, ngrp);
+
+  const bf16x8 z8 = bf16x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bf16x8 ones_row = col == 0 ? bf16x8{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f} : z8;   // V^T row 0 of tile 4
+  const char* kbase[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) kbase[ks] = Ks + col * 128 + (((ks * 4 + g) ^ ((col >> 1) & 7)) << 4);
+  const char* vbase[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+    vbase[dt] = Vs + (4 * g + (col >> 2)) * 128 + ((dt ^ ((2 * g + (col >> 3)) & 3)) << 5) + 8 * (col & 3);
+
+  // one pass over all keys for NT query tiles; wait_blocks: the first head's first pass waits per block for its
+  // DMA; release: after each block, barrier + stage that block of the next head (bn, hn)
+  auto run_pass = [&](auto ntc, const bf16x8 (&qf)[3][2], const int (&tl)[3], bool wait_blocks, bool release, int bn,
+                      int hn) {
+    constexpr int NT = decltype(ntc)::value;
+    float m_run[NT];
+    f32x4 acc[NT][NA];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      m_run[t] = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto do_block = [&](int c, auto tailc, auto firstc) {
+      constexpr bool TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
+      const int kvalid = L - c * 64;
+      f32x4 s[NT][4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) s[t][kt] = FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4(-m_run[t]);
+        if (TAIL && kt * 16 >= kvalid) continue;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbase[ks] + c * 8192 + kt * 2048);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kf, qf[t][ks], s[t][kt]);
+        }
+      }
+      if constexpr (TAIL) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (kt * 16 + g * 4 + j >= kvalid)
+#pragma unroll
+              for (int t = 0; t < NT; ++t) s[t][kt][j] = -INFINITY;
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4 m4 = s[t][0];
+#pragma unroll
+        for (int kt = 1; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) m4[j] = fmaxf(m4[j], s[t][kt][j]);
+        const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
+        if constexpr (FIRST) {
+          m_run[t] = cmax;
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= cmax;
+        } else if (__builtin_amdgcn_ballot_w64(cmax > RESCALE_THR)) {
+          const float d = cmax > RESCALE_THR ? cmax : 0.f;
+          const float alpha = __builtin_amdgcn_exp2f(-d);
+          m_run[t] += d;
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= d;
+#pragma unroll
+          for (int i = 0; i < NA; ++i) acc[t][i] *= alpha;
+        }
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(s[t][kt][j]);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (TAIL && kk * 32 >= kvalid) break;
+        bf16x8 pf[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pf[t][j] = (bf16)s[t][2 * kk][j];
+            pf[t][4 + j] = (bf16)s[t][2 * kk + 1][j];
+          }
+        bf16x8 vf[4];
+        lds_vt4(vbase[0] + c * 8192 + kk * 4096, vbase[1] + c * 8192 + kk * 4096, vbase[2] + c * 8192 + kk * 4096,
+                vbase[3] + c * 8192 + kk * 4096, vf);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf[dt], pf[t], acc[t][dt]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t][4] = mfma16x16x32(ones_row, pf[t], acc[t][4]);
+      }
+    };
+    auto block = [&](int c, auto tailc, auto firstc) {
+      if (wait_blocks) {
+        if (DEBUG == 0) wait_vmcnt_dyn(ops_after(c));
+        else if (DEBUG == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+      }
+      if (DEBUG != 1) do_block(c, tailc, firstc);
+      if (release) {   // every wave is done with block c: its rows take the next head's
+        bar();
+        stage(bn, hn, 8 * c, min(8 * c + 8, ngrp));
+      }
+    };
+    if (nfull > 0) block(0, std::false_type{}, std::true_type{});
+    else block(0, std::true_type{}, std::true_type{});
+    for (int c = 1; c < nfull; ++c) block(c, std::false_type{}, std::false_type{});
+    if (nfull < nch && nfull > 0) block(nfull, std::true_type{}, std::false_type{});
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float lsum = g == 0 ? acc[t][NA - 1][0] : 0.f;   // V^T row 0 of tile 4: lanes of k-group 0
+      const float inv = 1.0f / xrow_sum(lsum);
+      const int q = tl[t] * 16 + col;
+      if (q < L) {
+        bf16* orow = p.out + ((size_t)b * L + q) * p.ldo + h * DH;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const f32x4 v = acc[t][dt] * inv;
+          *reinterpret_cast<bf16x4*>(orow + dt * 16 + g * 4) = to_bf16x4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+  };
+
+  const float sl2 = p.scale * 1.4426950408889634f;
+  bool first_head = true;
+  for (;;) {
+    const int bhn = bh + gridDim.x;
+    const bool has_next = bhn < nbh;
+    const int bn = has_next ? bhn / p.H : 0, hn = has_next ? bhn - (bhn / p.H) * p.H : 0;
+    int start = 0;
+    for (int pass = 0; pass < npass; ++pass) {
+      const int nt = my_tiles / npass + (pass < my_tiles % npass ? 1 : 0);
+      const int tl[3] = {wave + NW * start, wave + NW * (start + (nt > 1 ? 1 : 0)), wave + NW * (start + (nt > 2 ? 2 : 0))};
+      start += nt;
+      bf16x8 qf[3][2];
+      if (first_head && pass == 0) {
+        if (DEBUG == 0) {
+          wait_vmcnt_dyn(ops_after(0));   // Q (the oldest loads) retire with block 0
+          asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]), "+v"(q0[2][0]), "+v"(q0[2][1]));
+        } else if (DEBUG == 1) {
+          asm volatile("s_waitcnt vmcnt(0)" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]),
+                       "+v"(q0[2][0]), "+v"(q0[2][1]));
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) qf[t][ks] = __builtin_bit_cast(bf16x8, q0[t][ks]);
+      } else {
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            qf[t][ks] = DEBUG == 2 ? bf16x8{} : *reinterpret_cast<const bf16x8*>(qptr(b, h, tl[t], ks));
+        // consumed in this branch: hipcc's waits for these loads stay here (see attention_v2_kernel)
+        asm volatile("" : "+v"(qf[0][0]), "+v"(qf[0][1]), "+v"(qf[1][0]), "+v"(qf[1][1]), "+v"(qf[2][0]), "+v"(qf[2][1]));
+      }
+      if (!p.q_log2) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) qf[t][ks] = scale_bf16x8(qf[t][ks], sl2);
+      }
+      const bool wait_blocks = first_head && pass == 0;
+      const bool release = has_next && pass == npass - 1;
+      if (nt == 3) run_pass(std::integral_constant<int, 3>{}, qf, tl, wait_blocks, release, bn, hn);
+      else if (nt == 2) run_pass(std::integral_constant<int, 2>{}, qf, tl, wait_blocks, release, bn, hn);
+      else run_pass(std::integral_constant<int, 1>{}, qf, tl, wait_blocks, release, bn, hn);
+    }
+    if (!has_next) break;
+    bh = bhn;
+    b = bn;
+    h = hn;
+    first_head = false;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's share of the next head (and its stores)
+    bar();                                             // everyone's
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Head-resident kernel for Dh = 72 (U-ViT-H/2 and H/4: libs/uvit.py:66-92 with embed_dim 1152, 16 heads), the
 // v2 structure above with the head dim cut as 64 + 8 instead of padded to 96:
 //   Q K^T: three v_mfma_f32_16x16x32_bf16 k-steps, the third over d 64..95 with d 64..71 in k-group 0 and the
@@ -672,19 +978,23 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
 //          q'k - m in log2 units (q carries Dh^-0.5 log2 e), ready for exp2;
 //   P V:   five 16-column output tiles (d 64..79 for the last; rows 73..79 of it are never stored and row 72, with
 //          V^T row 72 := ones, accumulates the softmax row sum).
-// K and V rows stay unpadded (144 B) so a head's K + V fit twice per CU at L = 258:
-//   LDS = [V rows 0 .. round8(L)) [K rows 0 .. round16(L)), 144 B each; staged by LDS-DMA as a flat array of
-//   16-B chunks (chunk ci -> row ci / 9, column chunk ci % 9).  PV reads whole 32-key steps, so V rows past
-//   round8(L) read the (finite) K rows behind them and are multiplied by P = 0; K rows past round8(L) are never
-//   staged and their scores are masked.  The 144-B stride leaves 2-way bank conflicts on the fragment reads
-//   (no 16-B chunk permutation of a 9-chunk row removes them; the MFMAs, not LDS, bound the loop).
+// K and V take 144 B per row (no padding) so a head's K + V fit twice per CU at L = 258:
+//   LDS = [V rows 0 .. round8(L), 144 B each] [K d 0..63: rows 0 .. round16(L), 128 B each] [K d 64..71: 16 B each].
+//   V is staged by LDS-DMA as a flat array of 16-B chunks (chunk ci -> row ci / 9, column chunk ci % 9); its
+//   transposed reads (8 B per lane) are nearly conflict-free at the 144-B stride.  K is split so the QK^T fragment
+//   reads (16 B per lane, 16 rows per LDS cycle) are conflict-free: d 0..63 as attention_v2_kernel's XOR-swizzled
+//   128-B rows, d 64..71 as a contiguous 16-B-per-row array (round 4's single 144-B K row gave every fragment read a
+//   2-way conflict: 0.45 conflict cycles per LDS cycle).  PV reads whole 32-key steps, so V rows past round8(L) read
+//   the (finite) K rows behind them and are multiplied by P = 0; K rows past L repeat row L - 1 and their scores
+//   are masked.
 template <int DEBUG>
 __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, int nqt, int LV, int L16) {
   constexpr int DH = 72, ROWB = 144, NCH = 9;
   constexpr float RESCALE_THR = 8.0f;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* Vs = lds;
-  char* Ks = lds + LV * ROWB;
+  char* Km = lds + LV * ROWB;   // K d 0..63, swizzled 128-B rows
+  char* Kt = Km + L16 * 128;     // K d 64..71, 16 B per row
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bh = blockIdx.x;
@@ -714,24 +1024,48 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
       q0r[t] = gload16_asm(qr + 64);
     }
   }
-  // K / V DMA: 64 chunks (1 KiB) per instruction, instruction i of each tensor issued by wave i % 4, V before K
-  const int ndma = (LV * NCH + 63) / 64;
-  if (DEBUG != 2) {
-    for (int i = wave; i < ndma; i += 4) {
-      const int ci = i * 64 + lane;
-      if (ci < LV * NCH) {
-        const int row = ci / NCH, ch = ci - row * NCH;
-        const bf16* src = base + (size_t)(row < L ? row : L - 1) * p.ldq + ch * 8;
-        glds16(src + 2 * D, (PDM_LDS void*)(Vs + i * 1024));
-        glds16(src + D, (PDM_LDS void*)(Ks + i * 1024));
-      }
+  // K / V DMA (1 KiB per instruction) in 64-key block order -- per block c: V instructions 9c .. 9c+8 (64 rows x 9
+  // chunks), K d 0..63 instructions 8c .. 8c+7 (8 rows each), the K d 64..71 instruction c (64 rows) -- dealt to the
+  // waves round robin over the whole list, so a block's instructions are all older than the next block's
+  const int ndmaV = (LV * NCH + 63) / 64, ndmaK = L16 / 8, nblk = (L16 + 63) / 64;
+  auto for_items = [&](auto&& fn) {   // fn(block, kind 0 V / 1 Km / 2 Kt, instruction) for this wave's items
+    int k = 0;
+    for (int c = 0; c < nblk; ++c) {
+      for (int i = 9 * c; i < min(9 * c + 9, ndmaV); ++i, ++k)
+        if ((k & 3) == wave) fn(c, 0, i);
+      for (int j = 8 * c; j < min(8 * c + 8, ndmaK); ++j, ++k)
+        if ((k & 3) == wave) fn(c, 1, j);
+      if ((k++ & 3) == wave) fn(c, 2, c);
     }
+  };
+  if (DEBUG != 2) {
+    const __amdgpu_buffer_rsrc_t rq = att_rsrc(p.qkv + (size_t)b * L * p.ldq, (long long)L * p.ldq * 2);
+    const int r8 = lane >> 3, pc = lane & 7;
+    for_items([&](int, int kind, int i) {
+      if (kind == 0) {
+        const int ci = i * 64 + lane;
+        if (ci < LV * NCH) {
+          const int row = ci / NCH, ch = ci - row * NCH;
+          att_dma16(rq, (unsigned)((row < L ? row : L - 1) * p.ldq + h * DH + 2 * D + ch * 8) * 2u,
+                    (PDM_LDS void*)(Vs + i * 1024));
+        }
+      } else if (kind == 1) {
+        const int row = i * 8 + r8;
+        const int kc = pc ^ ((row >> 1) & 7);
+        att_dma16(rq, (unsigned)((row < L ? row : L - 1) * p.ldq + h * DH + D + kc * 8) * 2u,
+                  (PDM_LDS void*)(Km + i * 1024));
+      } else {
+        const int row = i * 64 + lane;
+        if (row < L16)
+          att_dma16(rq, (unsigned)((row < L ? row : L - 1) * p.ldq + h * DH + D + 64) * 2u,
+                    (PDM_LDS void*)(Kt + i * 1024));
+      }
+    });
   }
-  // DMA instructions (both tensors) this wave issued past block c: rows < 64 (c + 1) are chunks < 576 (c + 1)
+  // DMA instructions this wave issued for blocks past c (the vmcnt that retires blocks 0 .. c and Q)
   auto ops_after = [&](int c) {
-    const int need = min(ndma, 9 * (c + 1));
     int n = 0;
-    for (int i = wave; i < ndma; i += 4) n += i >= need ? 2 : 0;
+    for_items([&](int blk, int, int) { n += blk > c ? 1 : 0; });
     return n;
   };
   auto block_ready = [&](int c) {
@@ -764,7 +1098,12 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
 #pragma unroll
       for (int i = 0; i < 5; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const char* kbase = Ks + col * ROWB;   // per-lane bases; block / kt / kk / dt offsets are immediates
+    // per-lane bases; block / kt / kk / dt offsets are immediates.  Swizzle of K row c*64 + kt*16 + col:
+    // ((row >> 1) & 7) = (col >> 1) & 7, independent of c and kt
+    const char* kbase[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) kbase[ks] = Km + col * 128 + (((ks * 4 + g) ^ ((col >> 1) & 7)) << 4);
+    const char* ktail = Kt + col * 16;
     const char* vbase = Vs + (4 * g + (col >> 2)) * ROWB + 8 * (col & 3);
     // log2-domain scores relative to the running max, as attention_v2_kernel
     auto do_block = [&](int c, auto tailc, auto firstc) {
@@ -774,18 +1113,17 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         if (TAIL && kt * 16 >= kvalid) continue;
-        const char* krow = kbase + c * (64 * ROWB) + kt * (16 * ROWB);
         // a third 16x16x32 step over d 64..95 carries d 64..71 (k-group 0) and, in the padding slot d = 72
         // (k-group 1), K = 1 against Q = -m_run, so the chain leaves q'k - m_run with no VALU pass over the scores
         // (one uniform MFMA chain: a 16x16x16 step chained with 16x16x32 ones got too few SrcC wait states
         // from hipcc on gfx950, measured wrong scores in both orders)
-        bf16x8 kx = *reinterpret_cast<const bf16x8*>(krow + 128);
+        bf16x8 kx = *reinterpret_cast<const bf16x8*>(ktail + c * 1024 + kt * 256);
         kx = g == 0 ? kx : (g == 1 ? one8 : zero8);
 #pragma unroll
         for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kx, qm[t], f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + (ks * 4 + g) * 16);
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbase[ks] + c * 8192 + kt * 2048);
 #pragma unroll
           for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kf, qf[t][ks], s[t][kt]);
         }
@@ -839,18 +1177,14 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
             pf[t][j] = (bf16)s[t][2 * kk][j];
             pf[t][4 + j] = (bf16)s[t][2 * kk + 1][j];
           }
-        const char* v1 = vbase + c * (64 * ROWB) + kk * (32 * ROWB);
-        const char* v2 = v1 + 16 * ROWB;
+        bf16x8 vf[5];
+        lds_vt5(vbase + c * (64 * ROWB) + kk * (32 * ROWB), vf);   // rows k and k + 16 (16 * ROWB = 2304)
+        // output row d = 72 (padding, never stored) becomes the softmax row sum: V^T row 72 := ones
+        vf[4] = (lane & 15) == 8 ? ones8 : vf[4];
 #pragma unroll
-        for (int dt = 0; dt < 5; ++dt) {
-          const s16x4 lo = lds_read_tr16(v1 + dt * 32);
-          const s16x4 hi = lds_read_tr16(v2 + dt * 32);
-          bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          // output row d = 72 (padding, never stored) becomes the softmax row sum: V^T row 72 := ones
-          if (dt == 4) vf = (lane & 15) == 8 ? ones8 : vf;
+        for (int dt = 0; dt < 5; ++dt)
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf, pf[t], acc[t][dt]);
-        }
+          for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf[dt], pf[t], acc[t][dt]);
       }
     };
     if (first) block_ready(0);
@@ -917,6 +1251,8 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(r + 64);
         qr[t] = g == 0 ? v : zero8;
       }
+      // consumed in this branch (see attention_v2_kernel)
+      asm volatile("" : "+v"(qf[0][0]), "+v"(qf[0][1]), "+v"(qf[1][0]), "+v"(qf[1][1]), "+v"(qr[0]), "+v"(qr[1]));
     }
     if (!p.q_log2) {   // q not pre-scaled by the producer: scale * log2(e) applied here (one extra bf16 rounding)
 #pragma unroll
@@ -928,6 +1264,292 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
     }
     if (two) run_pass(std::integral_constant<int, 2>{}, qf, qr, tl, pass == 0);
     else run_pass(std::integral_constant<int, 1>{}, qf, qr, tl, pass == 0);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Persistent Dh = 72 kernel (round 5): attention_h72_kernel's math and LDS layout, with attention_v3_kernel's head
+// loop -- the next head's K / V block c is staged right after the last pass releases block c -- and balanced, uniform
+// passes of 1-3 tiles.  DEBUG 1: loads only; 2: math only.
+template <int DEBUG>
+__global__ __launch_bounds__(256, 2) void attention_h72p_kernel(AttentionArgs p, int nqt, int LV, int L16) {
+  constexpr int DH = 72, ROWB = 144, NCH = 9, NW = 4;
+  constexpr float RESCALE_THR = 8.0f;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* Vs = lds;
+  char* Km = lds + LV * ROWB;   // K d 0..63, swizzled 128-B rows
+  char* Kt = Km + L16 * 128;     // K d 64..71, 16 B per row
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nbh = p.B * p.H, L = p.L, D = p.H * DH;
+  const int g = lane >> 4, col = lane & 15;
+  const bool glo = g < 2;   // output rows d 64..71 of the fifth PV tile (rows 72..79 are padding)
+  const int my_tiles = (nqt - wave + NW - 1) / NW;      // >= 1 (launched with nqt >= 4)
+  const int npass = ((nqt + NW - 1) / NW + 2) / 3;
+  const int nfull = L / 64, nch = (L + 63) / 64;
+  const int r8 = lane >> 3, pc = lane & 7;
+  // K / V DMA items per 64-key block c: V 9c .. 9c+8, K d 0..63 8c .. 8c+7, K d 64..71 c (18 per block, the last
+  // block possibly fewer), dealt round robin over the head's item list: item k of block c has k = 18c + local
+  const int ndmaV = (LV * NCH + 63) / 64, ndmaK = L16 / 8, nblk = (L16 + 63) / 64;
+  auto stage_block = [&](int b_, int h_, int c) {
+    if (DEBUG == 2) return;
+    const __amdgpu_buffer_rsrc_t rq = att_rsrc(p.qkv + (size_t)b_ * L * p.ldq, (long long)L * p.ldq * 2);
+    int k = 18 * c;
+    for (int i = 9 * c; i < min(9 * c + 9, ndmaV); ++i, ++k) {
+      if ((k & 3) != wave) continue;
+      const int ci = i * 64 + lane;
+      if (ci < LV * NCH) {
+        const int row = ci / NCH, ch = ci - row * NCH;
+        att_dma16(rq, (unsigned)((row < L ? row : L - 1) * p.ldq + h_ * DH + 2 * D + ch * 8) * 2u,
+                  (PDM_LDS void*)(Vs + i * 1024));
+      }
+    }
+    for (int j = 8 * c; j < min(8 * c + 8, ndmaK); ++j, ++k) {
+      if ((k & 3) != wave) continue;
+      const int row = j * 8 + r8;
+      const int kc = pc ^ ((row >> 1) & 7);
+      att_dma16(rq, (unsigned)((row < L ? row : L - 1) * p.ldq + h_ * DH + D + kc * 8) * 2u,
+                (PDM_LDS void*)(Km + j * 1024));
+    }
+    if ((k & 3) == wave) {
+      const int row = c * 64 + lane;
+      if (row < L16)
+        att_dma16(rq, (unsigned)((row < L ? row : L - 1) * p.ldq + h_ * DH + D + 64) * 2u, (PDM_LDS void*)(Kt + c * 1024));
+    }
+  };
+  auto items_in = [&](int c) {   // this wave's DMA items of block c
+    int n = 0, k = 18 * c;
+    for (int i = 9 * c; i < min(9 * c + 9, ndmaV); ++i, ++k) n += (k & 3) == wave;
+    for (int j = 8 * c; j < min(8 * c + 8, ndmaK); ++j, ++k) n += (k & 3) == wave;
+    return n + ((k & 3) == wave);
+  };
+  auto ops_after = [&](int c) {   // the first head: this wave's items of blocks past c
+    int n = 0;
+    for (int cc = c + 1; cc < nblk; ++cc) n += items_in(cc);
+    return n;
+  };
+  auto bar = []() {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  int bh = blockIdx.x;
+  int b = bh / p.H, h = bh - (bh / p.H) * p.H;
+  auto qrow = [&](int b_, int h_, int tile) {
+    int q = tile * 16 + col;
+    q = q < L ? q : L - 1;
+    return p.qkv + ((size_t)b_ * L + q) * p.ldq + h_ * DH;
+  };
+  const int nt0 = my_tiles / npass + (my_tiles % npass ? 1 : 0);
+  i32x4 q0[3][2], q0r[3];
+  if (DEBUG != 2) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const bf16* qr_ = qrow(b, h, wave + NW * min(t, nt0 - 1));
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) q0[t][ks] = gload16_asm(qr_ + ks * 32 + g * 8);
+      q0r[t] = gload16_asm(qr_ + 64);
+    }
+  }
+  for (int c = 0; c < nblk; ++c) stage_block(b, h, c);
+
+  const float sl2 = p.scale * 1.4426950408889634f;
+  const bf16x8 ones8 = bf16x8{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+  const bf16x8 one8 = bf16x8{1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bf16x8 zero8 = bf16x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const char* kbase[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) kbase[ks] = Km + col * 128 + (((ks * 4 + g) ^ ((col >> 1) & 7)) << 4);
+  const char* ktail = Kt + col * 16;
+  const char* vbase = Vs + (4 * g + (col >> 2)) * ROWB + 8 * (col & 3);
+
+  auto run_pass = [&](auto ntc, const bf16x8 (&qf)[3][2], const bf16x8 (&qr)[3], const int (&tl)[3], bool wait_blocks,
+                      bool release, int bn, int hn) {
+    constexpr int NT = decltype(ntc)::value;
+    float m_run[NT];
+    f32x4 acc[NT][5];
+    bf16x8 qm[NT];   // Q of the d 64..95 step: d 64..71 (k-group 0) and the slot d = 72 (k-group 1) = -m_run
+    auto set_qm = [&](int t) {
+      bf16x8 v = qr[t];
+      if (g == 1) v[0] = (bf16)(-m_run[t]);
+      qm[t] = v;
+    };
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      qm[t] = qr[t];
+      m_run[t] = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto do_block = [&](int c, auto tailc, auto firstc) {
+      constexpr bool TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
+      const int kvalid = L - c * 64;
+      f32x4 s[NT][4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        if (TAIL && kt * 16 >= kvalid) continue;
+        bf16x8 kx = *reinterpret_cast<const bf16x8*>(ktail + c * 1024 + kt * 256);
+        kx = g == 0 ? kx : (g == 1 ? one8 : zero8);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kx, qm[t], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbase[ks] + c * 8192 + kt * 2048);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kf, qf[t][ks], s[t][kt]);
+        }
+      }
+      if constexpr (TAIL) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (kt * 16 + g * 4 + j >= kvalid)
+#pragma unroll
+              for (int t = 0; t < NT; ++t) s[t][kt][j] = -INFINITY;
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4 m4 = s[t][0];
+#pragma unroll
+        for (int kt = 1; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) m4[j] = fmaxf(m4[j], s[t][kt][j]);
+        const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
+        if constexpr (FIRST) {
+          m_run[t] = (float)(bf16)cmax;
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= m_run[t];
+          set_qm(t);
+        } else if (__builtin_amdgcn_ballot_w64(cmax > RESCALE_THR)) {
+          const float d = cmax > RESCALE_THR ? (float)(bf16)(m_run[t] + cmax) - m_run[t] : 0.f;
+          const float alpha = __builtin_amdgcn_exp2f(-d);
+          m_run[t] += d;
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= d;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) acc[t][i] *= alpha;
+          set_qm(t);
+        }
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(s[t][kt][j]);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (TAIL && kk * 32 >= kvalid) break;
+        bf16x8 pf[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pf[t][j] = (bf16)s[t][2 * kk][j];
+            pf[t][4 + j] = (bf16)s[t][2 * kk + 1][j];
+          }
+        bf16x8 vf[5];
+        lds_vt5(vbase + c * (64 * ROWB) + kk * (32 * ROWB), vf);
+        vf[4] = (lane & 15) == 8 ? ones8 : vf[4];
+#pragma unroll
+        for (int dt = 0; dt < 5; ++dt)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf[dt], pf[t], acc[t][dt]);
+      }
+    };
+    auto block = [&](int c, auto tailc, auto firstc) {
+      if (wait_blocks) {
+        if (DEBUG == 0) wait_vmcnt_dyn(ops_after(c));
+        else if (DEBUG == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+      }
+      if (DEBUG != 1) do_block(c, tailc, firstc);
+      if (release) {   // every wave is done with block c: its rows take the next head's
+        bar();
+        stage_block(bn, hn, c);
+      }
+    };
+    if (nfull > 0) block(0, std::false_type{}, std::true_type{});
+    else block(0, std::true_type{}, std::true_type{});
+    for (int c = 1; c < nfull; ++c) block(c, std::false_type{}, std::false_type{});
+    if (nfull < nch && nfull > 0) block(nfull, std::true_type{}, std::false_type{});
+    // blocks staged but never read as their own block (V / K rows past the last 64-key block that holds keys)
+    if (release)
+      for (int c = nch; c < nblk; ++c) stage_block(bn, hn, c);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float inv = 1.0f / xrow_sum(g == 2 ? acc[t][4][0] : 0.f);   // row d = 72: lanes of k-group 2, j = 0
+      const int q = tl[t] * 16 + col;
+      if (q < L) {
+        bf16* orow = p.out + ((size_t)b * L + q) * p.ldo + h * DH;
+#pragma unroll
+        for (int dt = 0; dt < 5; ++dt) {
+          if (dt == 4 && !glo) break;
+          const f32x4 v = acc[t][dt] * inv;
+          *reinterpret_cast<bf16x4*>(orow + dt * 16 + g * 4) = to_bf16x4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+  };
+
+  bool first_head = true;
+  for (;;) {
+    const int bhn = bh + gridDim.x;
+    const bool has_next = bhn < nbh;
+    const int bn = has_next ? bhn / p.H : 0, hn = has_next ? bhn - (bhn / p.H) * p.H : 0;
+    int start = 0;
+    for (int pass = 0; pass < npass; ++pass) {
+      const int nt = my_tiles / npass + (pass < my_tiles % npass ? 1 : 0);
+      const int tl[3] = {wave + NW * start, wave + NW * (start + (nt > 1 ? 1 : 0)), wave + NW * (start + (nt > 2 ? 2 : 0))};
+      start += nt;
+      bf16x8 qf[3][2], qr[3];
+      if (first_head && pass == 0) {
+        if (DEBUG == 0) {
+          wait_vmcnt_dyn(ops_after(0));
+          asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]), "+v"(q0[2][0]), "+v"(q0[2][1]),
+                       "+v"(q0r[0]), "+v"(q0r[1]), "+v"(q0r[2]));
+        } else if (DEBUG == 1) {
+          asm volatile("s_waitcnt vmcnt(0)" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]),
+                       "+v"(q0[2][0]), "+v"(q0[2][1]), "+v"(q0r[0]), "+v"(q0r[1]), "+v"(q0r[2]));
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) qf[t][ks] = __builtin_bit_cast(bf16x8, q0[t][ks]);
+          qr[t] = g == 0 ? __builtin_bit_cast(bf16x8, q0r[t]) : zero8;
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const bf16* r = qrow(b, h, tl[t]);
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) qf[t][ks] = DEBUG == 2 ? zero8 : *reinterpret_cast<const bf16x8*>(r + ks * 32 + g * 8);
+          const bf16x8 v = DEBUG == 2 ? zero8 : *reinterpret_cast<const bf16x8*>(r + 64);
+          qr[t] = g == 0 ? v : zero8;
+        }
+        asm volatile("" : "+v"(qf[0][0]), "+v"(qf[0][1]), "+v"(qf[1][0]), "+v"(qf[1][1]), "+v"(qf[2][0]), "+v"(qf[2][1]),
+                     "+v"(qr[0]), "+v"(qr[1]), "+v"(qr[2]));
+      }
+      if (!p.q_log2) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) qf[t][ks] = scale_bf16x8(qf[t][ks], sl2);
+          qr[t] = scale_bf16x8(qr[t], sl2);
+        }
+      }
+      const bool wait_blocks = first_head && pass == 0;
+      const bool release = has_next && pass == npass - 1;
+      if (nt == 3) run_pass(std::integral_constant<int, 3>{}, qf, qr, tl, wait_blocks, release, bn, hn);
+      else if (nt == 2) run_pass(std::integral_constant<int, 2>{}, qf, qr, tl, wait_blocks, release, bn, hn);
+      else run_pass(std::integral_constant<int, 1>{}, qf, qr, tl, wait_blocks, release, bn, hn);
+    }
+    if (!has_next) break;
+    bh = bhn;
+    b = bn;
+    h = hn;
+    first_head = false;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
   }
 }
 }  // namespace
@@ -954,6 +1576,27 @@ hipError_t attention_launch(const AttentionArgs& args, hipStream_t stream) {
   // variants (normal / loads only / math only); measured tools/attn_bench.py
   const int LV = (p.L + 7) / 8 * 8, L16 = (p.L + 15) / 16 * 16;
   const int smem72 = (LV + L16) * 144;   // V rows read past LV (up to round32(L)) alias staged K rows below LV
+  // persistent Dh = 72 (14; 15 / 16 = loads-only / math-only timing): every wave owns a tile (nqt >= 4)
+  if (p.Dh == 72 && smem72 <= 80 * 1024 && (p.L + 31) / 32 * 32 <= 2 * LV && algo >= 14 && algo <= 16 && nqt >= 4) {
+    static bool attr72p = false;
+    static int ncu = 256;
+    if (!attr72p) {
+      (void)hipFuncSetAttribute((const void*)attention_h72p_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_h72p_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_h72p_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+        ncu = n;
+      attr72p = true;
+    }
+    const int nbh = p.B * p.H, slots = 2 * ncu;
+    const dim3 grid(nbh < slots ? nbh : slots), block(256);
+    if (algo == 15) hipLaunchKernelGGL(attention_h72p_kernel<1>, grid, block, smem72, stream, p, nqt, LV, L16);
+    else if (algo == 16) hipLaunchKernelGGL(attention_h72p_kernel<2>, grid, block, smem72, stream, p, nqt, LV, L16);
+    else hipLaunchKernelGGL(attention_h72p_kernel<0>, grid, block, smem72, stream, p, nqt, LV, L16);
+    return hipGetLastError();
+  }
+  if (algo >= 14 && algo <= 16) algo = p.Dh == 72 ? 7 : 0;
   if (p.Dh == 72 && smem72 <= 80 * 1024 && (p.L + 31) / 32 * 32 <= 2 * LV && (algo == 0 || (algo >= 7 && algo <= 9))) {
     static bool attr72 = false;
     if (!attr72) {
@@ -967,6 +1610,40 @@ hipError_t attention_launch(const AttentionArgs& args, hipStream_t stream) {
     else if (algo == 9) hipLaunchKernelGGL(attention_h72_kernel<2>, grid, block, smem72, stream, p, nqt, LV, L16);
     else hipLaunchKernelGGL(attention_h72_kernel<0>, grid, block, smem72, stream, p, nqt, LV, L16);
     return hipGetLastError();
+  }
+  // persistent v3 (11; 12 / 13 = loads-only / math-only timing): Dh = 64, every wave owns a tile (nqt >= NW)
+  if (algo >= 11 && algo <= 13 && p.Dh == 64 && Lp * 256 <= 160 * 1024) {
+    const int smem = Lp * 256;
+    const int nw = smem <= 80 * 1024 ? 4 : 8;
+    if (nqt >= nw) {
+      static bool attr3 = false;
+      static int ncu = 256;
+      if (!attr3) {
+        (void)hipFuncSetAttribute((const void*)attention_v3_kernel<0, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)attention_v3_kernel<1, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)attention_v3_kernel<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)attention_v3_kernel<0, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)attention_v3_kernel<1, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)attention_v3_kernel<2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+          ncu = n;
+        attr3 = true;
+      }
+      const int nbh = p.B * p.H, slots = ncu * (nw == 4 ? 2 : 1);
+      const dim3 grid(nbh < slots ? nbh : slots);
+      if (nw == 4) {
+        if (algo == 11) hipLaunchKernelGGL((attention_v3_kernel<0, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
+        else if (algo == 12) hipLaunchKernelGGL((attention_v3_kernel<1, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
+        else hipLaunchKernelGGL((attention_v3_kernel<2, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
+      } else {
+        if (algo == 11) hipLaunchKernelGGL((attention_v3_kernel<0, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
+        else if (algo == 12) hipLaunchKernelGGL((attention_v3_kernel<1, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
+        else hipLaunchKernelGGL((attention_v3_kernel<2, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
+      }
+      return hipGetLastError();
+    }
+    algo = 4;
   }
   if (p.Dh != 64 || Lp * 256 > 160 * 1024) algo = 1;
   // automatic: the head-resident v2 structure wherever the head's K/V fit in LDS (Dh = 64: every U-ViT-S/M/L

@@ -930,8 +930,9 @@ int pdm_set_gemm_tuning(int raster, int dbg_tile0) {
 }
 
 int pdm_set_attention_algo(int algo) {
-  if (algo < 0 || algo > 10)
-    return fail(PDM_ERR_ARG, "pdm_set_attention_algo: algo must be 0 (auto) or 1..10 (5, 6, 8, 9: timing experiments)");
+  if (algo < 0 || algo > 16)
+    return fail(PDM_ERR_ARG, "pdm_set_attention_algo: algo must be 0 (auto) or 1..16 (5, 6, 8, 9, 12, 13, 15, 16: timing "
+                             "experiments)");
   pdm::attention_set_algo(algo);
   return PDM_OK;
 }

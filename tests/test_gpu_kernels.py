@@ -398,13 +398,14 @@ def test_attention(lib, L, Dh, q_log2):
     assert rel(out.float(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4])
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 11])
 @pytest.mark.parametrize("L", [17, 32, 64, 66, 128, 129, 257, 258, 334, 513, 590])
 @pytest.mark.parametrize("ramp", [False, True])
 def test_attention_algos(lib, algo, L, ramp):
     """Both attention structures (1: streamed K/V per 64-query block; 2/3: head-resident K/V, 2 or 3 query
     tiles per wave; 4: head-resident v2, a ragged last tile at nqt = k NW + 1 (L = 66, 129, 257, 258, 513) run as the
-    third tile of a pass) at Dh = 64 on ragged lengths and whole 64-key blocks (the head-resident path declines shapes
+    third tile of a pass; 11: the persistent v3 streaming the next head's K/V, falling back to v2 below NW tiles) at
+    Dh = 64 on ragged lengths and whole 64-key blocks (the head-resident path declines shapes
     it cannot hold).  ramp: key magnitudes
     grow along the sequence, so later key blocks raise the running max past the deferred-rescale threshold."""
     H, B, Dh = 4, 3, 64
@@ -424,6 +425,61 @@ def test_attention_algos(lib, algo, L, ramp):
     ref = torch.softmax(q @ k.transpose(-1, -2) * Dh ** -0.5, dim=-1) @ v
     ref = ref.permute(0, 2, 1, 3).reshape(B * L, D)
     assert rel(out.float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,L,H", [(100, 258, 16), (50, 258, 16), (190, 258, 16), (7, 66, 100), (130, 66, 4),
+                                   (32, 334, 8), (32, 590, 8), (41, 128, 16), (64, 256, 16)])
+def test_attention_persistent_v3(lib, B, L, H):
+    """The persistent v3 kernel (algo 11: workgroups loop over heads and stream the next head's K/V into LDS during
+    their last pass) at the bench shapes, where every workgroup runs several heads (B*H > 2 x CUs), against fp32
+    torch and BIT-identical to the one-head-per-workgroup v2 (algo 4): a query tile's MFMA / exp chain does not
+    depend on the pass it runs in.  (7, 66, 100) and (130, 66, 4): one pass per head, so the first pass's per-block
+    waits and the release of each block for the next head run in the same pass."""
+    Dh = 64
+    D = H * Dh
+    g = torch.Generator(device="cuda").manual_seed(B * L + H)
+    qkv = torch.randn(B * L, 3 * D, device="cuda", generator=g) * 1.5
+    pos = torch.arange(B * L, device="cuda") % L
+    qkv[:, D:2 * D] *= (1 + 3 * pos / L)[:, None]   # later keys raise the running max (rescale branch)
+    qkv = qkv.bfloat16()
+    outs = {}
+    for algo in (4, 11):
+        lib.check(lib.load().pdm_set_attention_algo(algo), "pdm_set_attention_algo")
+        try:
+            outs[algo] = lib.attention(qkv, B, L, H, Dh)
+            torch.cuda.synchronize()
+        finally:
+            lib.load().pdm_set_attention_algo(0)
+    assert torch.equal(outs[11], outs[4])
+    q, k, v = qkv.float().reshape(B, L, 3, H, Dh).permute(2, 0, 3, 1, 4)
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v)
+    ref = ref.permute(0, 2, 1, 3).reshape(B * L, D)
+    assert rel(outs[11].float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,L", [(100, 258), (50, 258), (7, 66), (33, 130), (40, 257)])
+def test_attention_h72_persistent(lib, B, L):
+    """The persistent Dh = 72 kernel (algo 14) at the U-ViT-H head count with several heads per workgroup: fp32 torch
+    within 1e-2 and BIT-identical to the one-head-per-workgroup kernel (algo 7)."""
+    H, Dh = 16, 72
+    D = H * Dh
+    g = torch.Generator(device="cuda").manual_seed(B * L + 72)
+    qkv = torch.randn(B * L, 3 * D, device="cuda", generator=g) * 1.5
+    pos = torch.arange(B * L, device="cuda") % L
+    qkv[:, D:2 * D] *= (1 + 3 * pos / L)[:, None]
+    qkv = qkv.bfloat16()
+    outs = {}
+    for algo in (7, 14):
+        lib.check(lib.load().pdm_set_attention_algo(algo), "pdm_set_attention_algo")
+        try:
+            outs[algo] = lib.attention(qkv, B, L, H, Dh)
+            torch.cuda.synchronize()
+        finally:
+            lib.load().pdm_set_attention_algo(0)
+    assert torch.equal(outs[14], outs[7])
+    q, k, v = qkv.float().reshape(B, L, 3, H, Dh).permute(2, 0, 3, 1, 4)
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v).permute(0, 2, 1, 3).reshape(B * L, D)
+    assert rel(outs[14].float(), ref) < 1e-2
 
 
 @pytest.mark.parametrize("L", [33, 66, 129, 257, 258, 280])
