@@ -899,6 +899,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v3_kernel(
     else block(0, std::true_type{}, std::true_type{});
     for (int c = 1; c < nfull; ++c) block(c, std::false_type{}, std::false_type{});
     if (nfull < nch && nfull > 0) block(nfull, std::true_type{}, std::false_type{});
+    // (the next head's Q is not prefetched here by inline-asm loads: hipcc does not know such a load is in flight,
+    // and across this epilogue it may hand the destination registers to other values, which the late data then
+    // overwrites -- the likely cause of a GPU memory fault with that prefetch at 1600 heads, profiles/r05c)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const float lsum = g == 0 ? acc[t][NA - 1][0] : 0.f;   // V^T row 0 of tile 4: lanes of k-group 0
@@ -927,7 +930,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v3_kernel(
       const int tl[3] = {wave + NW * start, wave + NW * (start + (nt > 1 ? 1 : 0)), wave + NW * (start + (nt > 2 ? 2 : 0))};
       start += nt;
       bf16x8 qf[3][2];
-      if (first_head && pass == 0) {
+      if (first_head && pass == 0) {   // Q from the prologue
         if (DEBUG == 0) {
           wait_vmcnt_dyn(ops_after(0));   // Q (the oldest loads) retire with block 0
           asm volatile("" : "+v"(q0[0][0]), "+v"(q0[0][1]), "+v"(q0[1][0]), "+v"(q0[1][1]), "+v"(q0[2][0]), "+v"(q0[2][1]));
@@ -978,23 +981,24 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v3_kernel(
 //          q'k - m in log2 units (q carries Dh^-0.5 log2 e), ready for exp2;
 //   P V:   five 16-column output tiles (d 64..79 for the last; rows 73..79 of it are never stored and row 72, with
 //          V^T row 72 := ones, accumulates the softmax row sum).
-// K and V take 144 B per row (no padding) so a head's K + V fit twice per CU at L = 258:
-//   LDS = [V rows 0 .. round8(L), 144 B each] [K d 0..63: rows 0 .. round16(L), 128 B each] [K d 64..71: 16 B each].
-//   V is staged by LDS-DMA as a flat array of 16-B chunks (chunk ci -> row ci / 9, column chunk ci % 9); its
-//   transposed reads (8 B per lane) are nearly conflict-free at the 144-B stride.  K is split so the QK^T fragment
-//   reads (16 B per lane, 16 rows per LDS cycle) are conflict-free: d 0..63 as attention_v2_kernel's XOR-swizzled
-//   128-B rows, d 64..71 as a contiguous 16-B-per-row array (round 4's single 144-B K row gave every fragment read a
-//   2-way conflict: 0.45 conflict cycles per LDS cycle).  PV reads whole 32-key steps, so V rows past round8(L) read
-//   the (finite) K rows behind them and are multiplied by P = 0; K rows past L repeat row L - 1 and their scores
-//   are masked.
+// K and V rows stay unpadded (144 B) so a head's K + V fit twice per CU at L = 258:
+//   LDS = [V rows 0 .. round8(L)) [K rows 0 .. round16(L)), 144 B each; staged by LDS-DMA as a flat array of
+//   16-B chunks (chunk ci -> row ci / 9, column chunk ci % 9).  PV reads whole 32-key steps, so V rows past
+//   round8(L) read the (finite) K rows behind them and are multiplied by P = 0; K rows past round8(L) are never
+//   staged and their scores are masked.  The 144-B stride leaves 2-way bank conflicts on the fragment reads
+//   (no 16-B chunk permutation of a 9-chunk row removes them; the MFMAs, not LDS, bound the loop).
+// Measured against round 5's variants of this kernel (profiles/r05e/attn_h72_variants.log, same box): staging K / V
+// by buffer LDS-DMA with per-block counted waits, K split into swizzled 128-B rows + a 16-B tail array and V^T read
+// by one asm statement took 122-126 us at 100 rows (this kernel 104) and 74-76 us at 50 rows (60): the conflict-free
+// K reads saved 2 % of the math, the 64 scattered 16-B tail reads per block cost more in the loads, so the global
+// DMA form and the 144-B rows stay here (attention_h72p_kernel, algo 14, is the persistent variant of the new layout).
 template <int DEBUG>
 __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, int nqt, int LV, int L16) {
   constexpr int DH = 72, ROWB = 144, NCH = 9;
   constexpr float RESCALE_THR = 8.0f;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* Vs = lds;
-  char* Km = lds + LV * ROWB;   // K d 0..63, swizzled 128-B rows
-  char* Kt = Km + L16 * 128;     // K d 64..71, 16 B per row
+  char* Ks = lds + LV * ROWB;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bh = blockIdx.x;
@@ -1024,48 +1028,24 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
       q0r[t] = gload16_asm(qr + 64);
     }
   }
-  // K / V DMA (1 KiB per instruction) in 64-key block order -- per block c: V instructions 9c .. 9c+8 (64 rows x 9
-  // chunks), K d 0..63 instructions 8c .. 8c+7 (8 rows each), the K d 64..71 instruction c (64 rows) -- dealt to the
-  // waves round robin over the whole list, so a block's instructions are all older than the next block's
-  const int ndmaV = (LV * NCH + 63) / 64, ndmaK = L16 / 8, nblk = (L16 + 63) / 64;
-  auto for_items = [&](auto&& fn) {   // fn(block, kind 0 V / 1 Km / 2 Kt, instruction) for this wave's items
-    int k = 0;
-    for (int c = 0; c < nblk; ++c) {
-      for (int i = 9 * c; i < min(9 * c + 9, ndmaV); ++i, ++k)
-        if ((k & 3) == wave) fn(c, 0, i);
-      for (int j = 8 * c; j < min(8 * c + 8, ndmaK); ++j, ++k)
-        if ((k & 3) == wave) fn(c, 1, j);
-      if ((k++ & 3) == wave) fn(c, 2, c);
-    }
-  };
+  // K / V DMA: 64 chunks (1 KiB) per instruction, instruction i of each tensor issued by wave i % 4, V before K
+  const int ndma = (LV * NCH + 63) / 64;
   if (DEBUG != 2) {
-    const __amdgpu_buffer_rsrc_t rq = att_rsrc(p.qkv + (size_t)b * L * p.ldq, (long long)L * p.ldq * 2);
-    const int r8 = lane >> 3, pc = lane & 7;
-    for_items([&](int, int kind, int i) {
-      if (kind == 0) {
-        const int ci = i * 64 + lane;
-        if (ci < LV * NCH) {
-          const int row = ci / NCH, ch = ci - row * NCH;
-          att_dma16(rq, (unsigned)((row < L ? row : L - 1) * p.ldq + h * DH + 2 * D + ch * 8) * 2u,
-                    (PDM_LDS void*)(Vs + i * 1024));
-        }
-      } else if (kind == 1) {
-        const int row = i * 8 + r8;
-        const int kc = pc ^ ((row >> 1) & 7);
-        att_dma16(rq, (unsigned)((row < L ? row : L - 1) * p.ldq + h * DH + D + kc * 8) * 2u,
-                  (PDM_LDS void*)(Km + i * 1024));
-      } else {
-        const int row = i * 64 + lane;
-        if (row < L16)
-          att_dma16(rq, (unsigned)((row < L ? row : L - 1) * p.ldq + h * DH + D + 64) * 2u,
-                    (PDM_LDS void*)(Kt + i * 1024));
+    for (int i = wave; i < ndma; i += 4) {
+      const int ci = i * 64 + lane;
+      if (ci < LV * NCH) {
+        const int row = ci / NCH, ch = ci - row * NCH;
+        const bf16* src = base + (size_t)(row < L ? row : L - 1) * p.ldq + ch * 8;
+        glds16(src + 2 * D, (PDM_LDS void*)(Vs + i * 1024));
+        glds16(src + D, (PDM_LDS void*)(Ks + i * 1024));
       }
-    });
+    }
   }
-  // DMA instructions this wave issued for blocks past c (the vmcnt that retires blocks 0 .. c and Q)
+  // DMA instructions (both tensors) this wave issued past block c: rows < 64 (c + 1) are chunks < 576 (c + 1)
   auto ops_after = [&](int c) {
+    const int need = min(ndma, 9 * (c + 1));
     int n = 0;
-    for_items([&](int blk, int, int) { n += blk > c ? 1 : 0; });
+    for (int i = wave; i < ndma; i += 4) n += i >= need ? 2 : 0;
     return n;
   };
   auto block_ready = [&](int c) {
@@ -1098,12 +1078,7 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
 #pragma unroll
       for (int i = 0; i < 5; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    // per-lane bases; block / kt / kk / dt offsets are immediates.  Swizzle of K row c*64 + kt*16 + col:
-    // ((row >> 1) & 7) = (col >> 1) & 7, independent of c and kt
-    const char* kbase[2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) kbase[ks] = Km + col * 128 + (((ks * 4 + g) ^ ((col >> 1) & 7)) << 4);
-    const char* ktail = Kt + col * 16;
+    const char* kbase = Ks + col * ROWB;   // per-lane bases; block / kt / kk / dt offsets are immediates
     const char* vbase = Vs + (4 * g + (col >> 2)) * ROWB + 8 * (col & 3);
     // log2-domain scores relative to the running max, as attention_v2_kernel
     auto do_block = [&](int c, auto tailc, auto firstc) {
@@ -1113,17 +1088,18 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         if (TAIL && kt * 16 >= kvalid) continue;
+        const char* krow = kbase + c * (64 * ROWB) + kt * (16 * ROWB);
         // a third 16x16x32 step over d 64..95 carries d 64..71 (k-group 0) and, in the padding slot d = 72
         // (k-group 1), K = 1 against Q = -m_run, so the chain leaves q'k - m_run with no VALU pass over the scores
         // (one uniform MFMA chain: a 16x16x16 step chained with 16x16x32 ones got too few SrcC wait states
         // from hipcc on gfx950, measured wrong scores in both orders)
-        bf16x8 kx = *reinterpret_cast<const bf16x8*>(ktail + c * 1024 + kt * 256);
+        bf16x8 kx = *reinterpret_cast<const bf16x8*>(krow + 128);
         kx = g == 0 ? kx : (g == 1 ? one8 : zero8);
 #pragma unroll
         for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kx, qm[t], f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbase[ks] + c * 8192 + kt * 2048);
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + (ks * 4 + g) * 16);
 #pragma unroll
           for (int t = 0; t < NT; ++t) s[t][kt] = mfma16x16x32(kf, qf[t][ks], s[t][kt]);
         }
@@ -1177,14 +1153,18 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
             pf[t][j] = (bf16)s[t][2 * kk][j];
             pf[t][4 + j] = (bf16)s[t][2 * kk + 1][j];
           }
-        bf16x8 vf[5];
-        lds_vt5(vbase + c * (64 * ROWB) + kk * (32 * ROWB), vf);   // rows k and k + 16 (16 * ROWB = 2304)
-        // output row d = 72 (padding, never stored) becomes the softmax row sum: V^T row 72 := ones
-        vf[4] = (lane & 15) == 8 ? ones8 : vf[4];
+        const char* v1 = vbase + c * (64 * ROWB) + kk * (32 * ROWB);
+        const char* v2 = v1 + 16 * ROWB;
 #pragma unroll
-        for (int dt = 0; dt < 5; ++dt)
+        for (int dt = 0; dt < 5; ++dt) {
+          const s16x4 lo = lds_read_tr16(v1 + dt * 32);
+          const s16x4 hi = lds_read_tr16(v2 + dt * 32);
+          bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          // output row d = 72 (padding, never stored) becomes the softmax row sum: V^T row 72 := ones
+          if (dt == 4) vf = (lane & 15) == 8 ? ones8 : vf;
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf[dt], pf[t], acc[t][dt]);
+          for (int t = 0; t < NT; ++t) acc[t][dt] = mfma16x16x32(vf, pf[t], acc[t][dt]);
+        }
       }
     };
     if (first) block_ready(0);
@@ -1472,9 +1452,7 @@ __global__ __launch_bounds__(256, 2) void attention_h72p_kernel(AttentionArgs p,
     else block(0, std::true_type{}, std::true_type{});
     for (int c = 1; c < nfull; ++c) block(c, std::false_type{}, std::false_type{});
     if (nfull < nch && nfull > 0) block(nfull, std::true_type{}, std::false_type{});
-    // blocks staged but never read as their own block (V / K rows past the last 64-key block that holds keys)
-    if (release)
-      for (int c = nch; c < nblk; ++c) stage_block(bn, hn, c);
+    // (no prefetch of the next head's Q here as in attention_v3_kernel: held across the passes it spills at NT = 3)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const float inv = 1.0f / xrow_sum(g == 2 ? acc[t][4][0] : 0.f);   // row d = 72: lanes of k-group 2, j = 0
@@ -1611,7 +1589,10 @@ hipError_t attention_launch(const AttentionArgs& args, hipStream_t stream) {
     else hipLaunchKernelGGL(attention_h72_kernel<0>, grid, block, smem72, stream, p, nqt, LV, L16);
     return hipGetLastError();
   }
-  // persistent v3 (11; 12 / 13 = loads-only / math-only timing): Dh = 64, every wave owns a tile (nqt >= NW)
+  // persistent v3 (11; 12 / 13 = loads-only / math-only timing): Dh = 64, every wave owns a tile (nqt >= NW).  The
+  // automatic choice wherever it applies: L/2 at 100 rows 76.4 -> 66.6 us, 190 rows 143.5 -> 136.5, 50 rows 44.8 ->
+  // 44.0, t2i 334 / 590 unchanged (tools/attn_bench.py, profiles/r05d/attn.log)
+  if (algo == 0 && p.Dh == 64 && Lp * 256 <= 160 * 1024) algo = 11;
   if (algo >= 11 && algo <= 13 && p.Dh == 64 && Lp * 256 <= 160 * 1024) {
     const int smem = Lp * 256;
     const int nw = smem <= 80 * 1024 ? 4 : 8;
