@@ -214,6 +214,14 @@ typedef struct pdm_gemm_args {
   /* epi = 2 with accumulate: the fp32 residual is read from res_f32 [M][ldrf] instead of out_f32 (out of place:
    * out_f32 = res_f32 + A W^T + bias); null = in place */
   const float* res_f32; int ldrf;
+  /* row gather of A1: row m of the product reads A1 row (m / a_rows_per_group) * a_group_stride + m %
+   * a_rows_per_group (0: contiguous) -- the t2i injection reads the image rows of the mask-stream output */
+  int a_rows_per_group; int a_group_stride;
+  /* epi = 3: second output of the rounded rows at out2 row (m / out2_rows_per_group) * out2_group_stride + m %
+   * out2_rows_per_group (stride ldo) and, with stats_out, their LayerNorm partials at the same row of stats_out2
+   * (libs/uvit_t2i.py:426/443/459: the new x straight into the image half of the next mask-stream input) */
+  void* out2; int out2_rows_per_group; int out2_group_stride;
+  float* stats_out2;
 } pdm_gemm_args;
 int pdm_gemm(const pdm_gemm_args* a, int epi, void* stream);
 /* Two GEMMs with the same epilogue, N, K and strides (different operands, rows and outputs) as ONE grouped launch of

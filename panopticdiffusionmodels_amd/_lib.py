@@ -65,6 +65,9 @@ class PdmGemmArgs(ctypes.Structure):
         ("mx_center", ctypes.c_int), ("ln_gcol", ctypes.c_void_p),
         ("res_in", ctypes.c_void_p), ("ldri", ctypes.c_int),
         ("res_f32", ctypes.c_void_p), ("ldrf", ctypes.c_int),
+        ("a_rows_per_group", ctypes.c_int), ("a_group_stride", ctypes.c_int),
+        ("out2", ctypes.c_void_p), ("out2_rows_per_group", ctypes.c_int), ("out2_group_stride", ctypes.c_int),
+        ("stats_out2", ctypes.c_void_p),
     ]
 
 
@@ -347,7 +350,8 @@ def gemm_pair(epi, first, second):
 
 def _gemm_args(a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=None, accumulate=False,
                ln_stats=None, ln_colsum=None, stats_out=None, out_fp8=None, out_scale=None, eps=1e-5,
-               mx_center=False, ln_gcol=None, res_in=None, res_f32=None, a2=None):
+               mx_center=False, ln_gcol=None, res_in=None, res_f32=None, a2=None, a_gather=None, out2=None,
+               out2_gather=None, stats_out2=None):
     require_gpu(a)
     M, K = a.shape
     N = w.shape[0]
@@ -382,6 +386,12 @@ def _gemm_args(a, w, bias=None, a_scale=None, w_scale=None, out=None, out_f32=No
         g.res_in, g.ldri = res_in.data_ptr(), res_in.stride(0)
     if res_f32 is not None:
         g.res_f32, g.ldrf = res_f32.data_ptr(), res_f32.stride(0)
+    if a_gather is not None:   # (M, rows_per_group, group_stride): row m reads a[(m // rpg) * gs + m % rpg]
+        g.M, g.a_rows_per_group, g.a_group_stride = a_gather
+    if out2 is not None:       # out2_gather = (rows_per_group, group_stride) of the second residual output
+        g.out2 = out2.data_ptr()
+        g.out2_rows_per_group, g.out2_group_stride = out2_gather
+        g.stats_out2 = stats_out2.data_ptr() if stats_out2 is not None else None
     return g
 
 

@@ -818,12 +818,15 @@ int t2i_two_stream16(const Ctx& c, const Workspace& w, int rows, int use_ground_
   };
   // mb = cat(x_img, m_src[:, Lx:]) + its partials (m_src == MB: the mask rows are already in place).  The mask
   // rows' LayerNorm partials are already in STM (written there by the mask block that produced m_src, in its fc2
-  // epilogue, or by the token assembly); the image rows' are x's own (ST, from the injection GEMM / the assembly).
-  auto refresh = [&](const bf16* x_img, const bf16* m_src) -> int {
-    PDM_TRY(copy_rows(w.MB, x_img, Lx, Lm, Lx, w.STM, w.ST));
+  // epilogue, or by the token assembly).  The image rows and their partials come from the injection GEMM's second
+  // output (img_in_place), and only before the first layer from x itself (XB / ST of the assembly).
+  auto refresh = [&](const bf16* x_img, const bf16* m_src, bool img_in_place) -> int {
+    if (!img_in_place) PDM_TRY(copy_rows(w.MB, x_img, Lx, Lm, Lx, w.STM, w.ST));
     if (m_src != w.MB) PDM_TRY(copy_rows(w.MB + (size_t)Lx * D, m_src + (size_t)Lx * D, Lm - Lx, Lm, Lm));
     return PDM_OK;
   };
+  // x_out = x_res + zeroconv(mout[:, :Lx]), also stored (with its partials) as the image rows of MB -- the next
+  // layer's mask-stream input; mout (SKM[i] / MXB) is never MB, so no tile reads rows another one writes
   auto inject = [&](int layer, const bf16* mout, const bf16* x_res, bf16* x_out) -> int {
     const std::string zc = "zero_convs." + std::to_string(2 * layer + 1) + ".conv";
     pdm::GemmArgs a{};
@@ -834,6 +837,8 @@ int t2i_two_stream16(const Ctx& c, const Workspace& w, int rows, int use_ground_
     a.out_bf16 = x_out; a.ldo = D;
     a.res_in = x_res; a.ldri = D; a.accumulate = 1;
     a.stats_out = w.ST; a.stats_ld = T;
+    a.out2 = w.MB; a.out2_rpg = Lx; a.out2_gs = Lm;
+    a.stats_out2 = w.STM;
     return launch_gemm(c, a, pdm::EPI_RES);
   };
   // image tokens -> XB + ST; mask tokens -> MB[:, Lx:] (the image rows of this pass are overwritten by refresh)
@@ -863,19 +868,19 @@ int t2i_two_stream16(const Ctx& c, const Workspace& w, int rows, int use_ground_
     return run_block16(c, ipre, rows, Lx, xin, w.ST, sk, w.XT, nullptr, w);
   };
   for (int i = 0; i < n; ++i, ++layer) {
-    PDM_TRY(refresh(x, m));
+    PDM_TRY(refresh(x, m, i > 0));
     PDM_TRY(blocks("in_blocks_mask." + std::to_string(i), "in_blocks." + std::to_string(i), nullptr, nullptr, x,
                    w.SKM + i * MDm));
     PDM_TRY(inject(layer, w.SKM + i * MDm, ximg, w.SK + i * MDx));
     x = w.SK + i * MDx;
     m = w.SKM + i * MDm;
   }
-  PDM_TRY(refresh(x, m));
+  PDM_TRY(refresh(x, m, n > 0));
   PDM_TRY(blocks("mid_block_mask", "mid_block", nullptr, nullptr, x, w.MXB));
   PDM_TRY(inject(layer, w.MXB, ximg, w.XB));
   ++layer;
   for (int i = 0; i < n; ++i, ++layer) {
-    PDM_TRY(refresh(w.XB, w.MXB));
+    PDM_TRY(refresh(w.XB, w.MXB, true));
     const bf16* skm = h->cfg.skip ? w.SKM + (n - 1 - i) * MDm : nullptr;
     const bf16* sk = h->cfg.skip ? w.SK + (n - 1 - i) * MDx : nullptr;
     PDM_TRY(blocks("out_blocks_mask." + std::to_string(i), "out_blocks." + std::to_string(i), skm, sk, w.XB, w.MXB));
@@ -1351,6 +1356,9 @@ static pdm::GemmArgs to_gemm_args(const pdm_gemm_args* g) {
   a.mx_center = g->mx_center; a.ln_gcol = (const bf16*)g->ln_gcol;
   a.res_in = (const bf16*)g->res_in; a.ldri = g->ldri;
   a.res_f32 = g->res_f32; a.ldrf = g->ldrf;
+  a.a_rows_per_group = g->a_rows_per_group; a.a_group_stride = g->a_group_stride;
+  a.out2 = (bf16*)g->out2; a.out2_rpg = g->out2_rows_per_group; a.out2_gs = g->out2_group_stride;
+  a.stats_out2 = g->stats_out2;
   return a;
 }
 

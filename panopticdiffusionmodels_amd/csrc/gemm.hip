@@ -405,8 +405,13 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
       q += n + 4 + j < p.N ? d1 * d1 : 0.f;
     }
     q = sum32(q);
-    if ((tid & 31) == 0 && m < p.M)
+    if ((tid & 31) == 0 && m < p.M) {
       *reinterpret_cast<float2*>(p.stats_out + ((size_t)m * p.stats_ld + (n0 >> 8)) * 2) = make_float2(sv, q);
+      if (EPI == EPI_RES && p.stats_out2) {
+        const size_t m2 = (size_t)(m / p.out2_rpg) * p.out2_gs + m % p.out2_rpg;
+        *reinterpret_cast<float2*>(p.stats_out2 + (m2 * p.stats_ld + (n0 >> 8)) * 2) = make_float2(sv, q);
+      }
+    }
     return mu;
   };
   // MXFP8 copy of the stored fp32 row piece, minus its 256-column group mean c (mx_center; 0 otherwise)
@@ -471,7 +476,11 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
           bf16x8 o;
 #pragma unroll
           for (int j = 0; j < 4; ++j) { o[j] = (bf16)v0[i][j]; o[4 + j] = (bf16)v1[i][j]; }
-          if (full || (m < p.M && n < p.N)) *reinterpret_cast<bf16x8*>(p.out_bf16 + (size_t)m * p.ldo + n) = o;
+          if (full || (m < p.M && n < p.N)) {
+            *reinterpret_cast<bf16x8*>(p.out_bf16 + (size_t)m * p.ldo + n) = o;
+            if (p.out2)
+              *reinterpret_cast<bf16x8*>(p.out2 + ((size_t)(m / p.out2_rpg) * p.out2_gs + m % p.out2_rpg) * p.ldo + n) = o;
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) { v0[i][j] = (float)o[j]; v1[i][j] = (float)o[4 + j]; }
         }
@@ -2537,6 +2546,8 @@ const char* gemm_check(const GemmArgs& p, int epi) {
   if (p.K % BK) return "gemm: K must be a multiple of 64";
   if (p.K1 % BK || p.K1 <= 0 || p.K1 > p.K) return "gemm: K1 must be a positive multiple of 64 and <= K";
   if (p.K1 < p.K && !p.A2) return "gemm: split-K operand A2 missing";
+  if (p.a_rows_per_group < 0 || (p.a_rows_per_group > 0 && p.a_group_stride < p.a_rows_per_group))
+    return "gemm: row gather needs a_group_stride >= a_rows_per_group";
   if (!p.A1 || !p.W) return "gemm: null operand";
   if ((p.lda1 % 8) || (p.K1 < p.K && (p.lda2 % 8))) return "gemm: lda must be a multiple of 8 (16-byte rows)";
   if (p.ldw && (p.ldw < p.K || p.ldw % 8)) return "gemm: ldw must be >= K and a multiple of 8";
@@ -2550,6 +2561,7 @@ const char* gemm_check(const GemmArgs& p, int epi) {
   if (p.stats_out && ((epi != EPI_F32 && epi != EPI_RES) || p.stats_ld < (p.N + 255) / 256 || ((uintptr_t)p.stats_out & 7)))
     return "gemm: LayerNorm stats need the fp32 / residual epilogue and stats_ld >= ceil(N / 256)";
   if ((p.stats_out || p.ln_stats) && p.batch > 1) return "gemm: fused LayerNorm is not available for batched GEMMs";
+  if ((p.out2 || p.stats_out2) && epi != EPI_RES) return "gemm: out2 / stats_out2 belong to the residual epilogue";
   if (p.out_fp8 && (p.N % 32 || p.ldo8 % 16 || !p.out_scale || p.out_scale_ld < p.M || p.batch > 1 ||
                     ((uintptr_t)p.out_fp8 & 15) || ((uintptr_t)p.out_scale & 3)))
     return "gemm: MXFP8 output needs N % 32 == 0, ldo8 % 16 == 0, a scale array with out_scale_ld >= M";
@@ -2578,6 +2590,9 @@ const char* gemm_check(const GemmArgs& p, int epi) {
     if (p.accumulate && (!p.res_in || p.ldri % 8 || ((uintptr_t)p.res_in & 15)))
       return "gemm(residual): accumulate needs res_in with ldri % 8 == 0, 16-byte aligned";
     if (p.N % 8 || p.batch > 1 || p.conv) return "gemm(residual): N % 8 == 0, no batch / conv";
+    if (p.out2 && (p.out2_rpg <= 0 || p.out2_gs < p.out2_rpg || ((uintptr_t)p.out2 & 15) || p.out_fp8 ||
+                   (p.stats_out2 && (!p.stats_out || ((uintptr_t)p.stats_out2 & 7)))))
+      return "gemm(residual): out2 needs 0 < out2_rpg <= out2_gs, 16-byte alignment, no MXFP8 output; stats_out2 needs stats_out";
   } else if (epi == EPI_F32) {
     if (!p.out_f32 || (p.ldr % 4)) return "gemm: f32 output missing or ldr not a multiple of 4";
     if (p.res_f32 && (!p.accumulate || p.ldrf % 4 || ((uintptr_t)p.res_f32 & 15) || p.batch > 1))
@@ -2827,7 +2842,7 @@ static bool fits_8s(const GemmArgs& p, int epi) {
   const long long lim = 0x7fffffffLL;
   if (!persist_kernels_ok()) return false;
   if (epi != EPI_BF16 && epi != EPI_GELU && epi != EPI_RES) return false;
-  if (p.conv || p.batch > 1 || p.a_rows_per_group > 0 || p.fp8 || p.mx_center) return false;
+  if (p.conv || p.batch > 1 || p.a_rows_per_group > 0 || p.fp8 || p.mx_center || p.out2) return false;
   if (p.out_fp8) {
     if (epi == EPI_RES || p.out_bf16 || !p.out_scale || p.N % 32 || p.ldo8 % 16 || p.out_scale_ld < p.M) return false;
     if ((long long)p.M * p.ldo8 >= lim || (long long)((p.N + 127) >> 7) * p.out_scale_ld * 4 >= lim) return false;
@@ -2880,6 +2895,14 @@ static bool fits_rsrc(const GemmArgs& p) {
   const long long a2 = p.A2 ? (long long)p.M * p.lda2 * 2 : 0;
   const long long w = (long long)p.N * (p.ldw > 0 ? p.ldw : p.K) * es;
   return a1 < lim && a2 < lim && w < lim && (!p.conv || p.convW < 4096);
+}
+
+// the second residual output of a launch whose kernel has no out2 store (the 128 tile, a split launch): the rows
+// (and partials) copied from out_bf16 / stats_out after it, as 4-byte words
+static hipError_t out2_copy(const GemmArgs& p, hipStream_t stream) {
+  return rowcopy_launch(reinterpret_cast<float*>(p.out2), p.ldo / 2, reinterpret_cast<const float*>(p.out_bf16),
+                        p.ldo / 2, p.M, p.N / 2, p.out2_rpg, p.out2_gs, p.out2_rpg, stream, p.stats_out2,
+                        p.stats_ld * 2, p.stats_out, p.stats_ld * 2, p.stats_out2 ? p.stats_ld * 2 : 0);
 }
 
 hipError_t gemm_launch_pair(const GemmArgs& a, const GemmArgs& b, int epi, hipStream_t stream) {
@@ -2948,6 +2971,8 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
       GemmArgs a = args, b = args;
       a.sk_flags = b.sk_flags = nullptr;   // one flag block serves one launch
       a.sk_slab = b.sk_slab = nullptr;
+      a.out2 = b.out2 = nullptr;           // the second output: one copy after both parts
+      a.stats_out2 = b.stats_out2 = nullptr;
       a.M = m1;
       b.M = p.M - m1;
       if (p.conv) b.A1 += (size_t)(m1 / hw) * (p.convH >> p.conv_up) * (p.convW >> p.conv_up) * p.convC;
@@ -2961,8 +2986,10 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
       if (b.res_f32) b.res_f32 += (size_t)m1 * p.ldrf;
       if (b.stats_out) b.stats_out += (size_t)m1 * p.stats_ld * 2;
       if (b.ln_stats) b.ln_stats += (size_t)m1 * p.ln_ld * 2;
-      const hipError_t e = gemm_launch(a, epi, stream);
-      return e != hipSuccess ? e : gemm_launch(b, epi, stream);
+      hipError_t e = gemm_launch(a, epi, stream);
+      if (e == hipSuccess) e = gemm_launch(b, epi, stream);
+      if (e == hipSuccess && p.out2) e = out2_copy(p, stream);
+      return e;
     }
   }
   if (algo == 8 && fits_rsrc(p)) return p.conv ? launch8d_hn<1>(p, epi, stream) : launch8d_hn<0>(p, epi, stream);
@@ -2997,6 +3024,7 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
     if (epi == EPI_RES) e = rowstats_bf16_launch(p.out_bf16, p.ldo, p.M, p.N, p.stats_out, p.stats_ld, stream);
     else e = rowstats_launch(p.out_f32, p.ldr, p.M, p.N, nullptr, 0, p.stats_out, p.stats_ld, stream);
   }
+  if (e == hipSuccess && epi == EPI_RES && p.out2) e = out2_copy(p, stream);
   return e;
 }
 

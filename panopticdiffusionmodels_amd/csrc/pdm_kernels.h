@@ -68,6 +68,12 @@ struct GemmArgs {
   // EPI_RES residual input [M][ldri] bf16 (may alias out_bf16: each element is read before it is written, by
   // the same thread)
   const bf16* res_in; int ldri;
+  // EPI_RES second output (the 256-tile epilogue): the rounded row m is also stored at out2 row
+  // (m / out2_rpg) * out2_gs + m % out2_rpg (stride ldo) and, with stats_out, its partials at the same row of
+  // stats_out2 (stride stats_ld) -- the t2i injection writes the new image tokens x straight into the image half of
+  // the next mask-stream input cat(x, m) (libs/uvit_t2i.py:426, 443, 459)
+  bf16* out2; int out2_rpg, out2_gs;
+  float* stats_out2;
   // EPI_F32 with accumulate: the residual is read from res_f32 [M][ldrf] instead of out_f32 (out of place:
   // out_f32 = res_f32 + A W^T + bias; the training forward keeps every block's input and output streams)
   const float* res_f32; int ldrf;

@@ -612,3 +612,49 @@ def test_gemm_pair_grouped_vs_separate(lib, case):
             res = o if case == "fc2_res_inplace" else kw["res_in"]
             want = a.float() @ kw["w"].float().t() + kw["bias"] + res.float()
             assert rel(kw["out"].float(), want) < 1e-2, case
+
+
+@pytest.mark.parametrize("G,Lx,Lm,algo", [(32, 334, 590, 0), (16, 334, 590, 0), (5, 70, 100, 0), (32, 334, 590, 1),
+                                          (3, 257, 300, 0)])
+def test_gemm_gather_second_output(lib, G, Lx, Lm, algo):
+    """The t2i injection GEMM (capi.hip t2i_two_stream16 inject): A rows gathered from the image rows of the mask
+    stream (row m -> (m // Lx) * Lm + m % Lx), EPI_RES with partials, and the second output writing the rounded rows
+    and their partials into the image rows of the next mask-stream input.  The product and partials are
+    BIT-identical to the same GEMM on a contiguous copy of the gathered rows; out2 / stats_out2 hold exactly out /
+    stats_out at the scattered rows and leave the mask rows untouched.  algo 1: the 128 tile (its out2 is a row
+    copy after the launch)."""
+    D = 512
+    g = torch.Generator(device="cuda").manual_seed(G * Lx + Lm)
+    src = torch.randn(G * Lm, D, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(D, D, device="cuda", generator=g) * D ** -0.5).bfloat16()
+    bias = torch.randn(D, device="cuda", generator=g)
+    res = torch.randn(G * Lx, D, device="cuda", generator=g).bfloat16()
+    M = G * Lx
+    idx = (torch.arange(M, device="cuda") // Lx) * Lm + torch.arange(M, device="cuda") % Lx
+    a_c = src[idx].contiguous()
+    out_ref = torch.empty(M, D, device="cuda", dtype=torch.bfloat16)
+    st_ref = torch.empty(M, 2, 2, device="cuda")
+    out = torch.empty_like(out_ref)
+    st = torch.empty_like(st_ref)
+    mb = torch.full((G * Lm, D), 7.0, device="cuda", dtype=torch.bfloat16)
+    stm = torch.full((G * Lm, 2, 2), -3.0, device="cuda")
+    # the reference on the kernel the gathered launch takes (the persistent kernel has no row gather: the 256 tile
+    # of algo 7, or the 128 tile below 4096 rows), whose partials come from the same reduction order
+    try:
+        lib.check(lib.load().pdm_set_gemm_algo(algo or (7 if M >= 4096 else 1)), "pdm_set_gemm_algo")
+        lib.gemm_ex(lib.EPI_RES, a_c, w, bias, out=out_ref, res_in=res, accumulate=True, stats_out=st_ref)
+        lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
+        lib.gemm_ex(lib.EPI_RES, src, w, bias, out=out, res_in=res, accumulate=True, stats_out=st,
+                    a_gather=(M, Lx, Lm), out2=mb, out2_gather=(Lx, Lm), stats_out2=stm)
+        torch.cuda.synchronize()
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+    ref = a_c.float() @ w.float().t() + bias + res.float()
+    assert rel(out_ref.float(), ref) < 1e-2
+    assert torch.equal(out, out_ref)
+    assert torch.equal(st, st_ref)
+    assert torch.equal(mb[idx], out)
+    assert torch.equal(stm[idx], st)
+    rest = torch.ones(G * Lm, dtype=torch.bool, device="cuda")
+    rest[idx] = False
+    assert bool((mb[rest] == 7.0).all()) and bool((stm[rest] == -3.0).all())
