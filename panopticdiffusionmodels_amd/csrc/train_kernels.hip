@@ -7,6 +7,7 @@
 //                      hardware transposing read ds_read_b64_tr_b16, so neither activation is ever transposed
 //                      in HBM.  The long reduction (M = tokens) is split over workgroups into fp32 partials.
 //   * attn_bwd_kernel  softmax attention backward for one (sequence, head) per workgroup, Q K V dO resident in LDS
+//                      (L <= 288) or two of them at a time (L <= 608: the t2i image / mask streams)
 //   * LayerNorm / GELU / bias / embedding / final conv / decoder_pred backward, the LSimple loss, AdamW + EMA.
 #include <algorithm>
 
@@ -377,31 +378,53 @@ __device__ __forceinline__ bf16x8 ab_trT(const char* img, int r0, int d0, int la
   return tr_frag(img + ab_off(ra, c) + (p & 1) * 8, img + ab_off(rb, c) + (p & 1) * 8);
 }
 
-__global__ __launch_bounds__(AB_THREADS, 1) void attn_bwd_kernel(AttnBwdArgs p) {
-  constexpr int NWV = AB_THREADS / 64;   // waves: 16 = four per SIMD (120 VGPRs each)
+// LONG = 1 (288 < L <= 608: the t2i streams, 334 image / 590 mask tokens): the four images do not fit, so LDS holds
+// two at a time -- Q and dO for pass 0 / pass A (a wave's own 16 keys' K and V rows sit in its registers; pass 0
+// reads K rows from global / L2), then K and V for pass B (a wave's own query's Q and dO rows in registers).  The
+// arithmetic (fragments, MFMA order, P / dS rounding) is the resident kernel's, so both give the same bits where
+// both apply; 8 waves (2 per SIMD) leave room for the register-resident rows.
+constexpr int AB_MAXL_LONG = 608;
+constexpr int AB_THREADS_LONG = 512;
+
+template <int LONG>
+__global__ __launch_bounds__(LONG ? AB_THREADS_LONG : AB_THREADS, 1) void attn_bwd_kernel(AttnBwdArgs p) {
+  constexpr int NTH = LONG ? AB_THREADS_LONG : AB_THREADS;
+  constexpr int NWV = NTH / 64;   // resident: 16 waves = four per SIMD (120 VGPRs each); LONG: 8
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = p.L, Lp = (L + 31) & ~31;
   const int bh = blockIdx.x, b = bh / p.H, h = bh - b * p.H;
   const int D = p.H * 64;
+  // resident: [Q | K | V | dO]; LONG: [Q | dO], later [K | V]
   char* Qs = smem;
-  char* Ks = Qs + Lp * 128;
-  char* Vs = Ks + Lp * 128;
-  char* Os = Vs + Lp * 128;   // dO
-  float* lse = reinterpret_cast<float*>(Os + Lp * 128);
+  char* Ks = LONG ? smem : Qs + Lp * 128;
+  char* Vs = LONG ? smem + Lp * 128 : Ks + Lp * 128;
+  char* Os = LONG ? smem + Lp * 128 : Vs + Lp * 128;   // dO
+  float* lse = reinterpret_cast<float*>(smem + (LONG ? 2 : 4) * Lp * 128);
   float* dlt = lse + Lp;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t row0 = (size_t)b * L;
-
-  // stage Q, K, V, dO (16-B chunks, rows >= L zero)
-  for (int e = tid; e < Lp * 8 * 4; e += AB_THREADS) {
-    const int img = e / (Lp * 8), r = (e / 8) % Lp, c = e & 7;
-    bf16x8 v = bf16x8{};
-    if (r < L) {
-      const bf16* src = img < 3 ? p.qkv + (row0 + r) * p.ldq + img * D + h * 64 + c * 8
-                                : p.dout + (row0 + r) * p.lddo + h * 64 + c * 8;
-      v = *reinterpret_cast<const bf16x8*>(src);
+  // global row r (clamped to the sequence) of image img: 0 Q, 1 K, 2 V, 3 dO; 16-B chunk c
+  auto grow = [&](int img, int r, int c) -> bf16x8 {
+    r = r < L ? r : L - 1;
+    const bf16* src = img < 3 ? p.qkv + (row0 + r) * p.ldq + img * D + h * 64 + c * 8
+                              : p.dout + (row0 + r) * p.lddo + h * 64 + c * 8;
+    return *reinterpret_cast<const bf16x8*>(src);
+  };
+  // stage images (16-B chunks, rows >= L zero): slot i of LDS <- image imgs[i]
+  auto stage = [&](int n, const int* imgs) {
+    for (int e = tid; e < Lp * 8 * n; e += NTH) {
+      const int i = e / (Lp * 8), r = (e / 8) % Lp, c = e & 7;
+      bf16x8 v = bf16x8{};
+      if (r < L) v = grow(imgs[i], r, c);
+      *reinterpret_cast<bf16x8*>(smem + i * Lp * 128 + ab_off(r, c)) = v;
     }
-    *reinterpret_cast<bf16x8*>(smem + img * Lp * 128 + ab_off(r, c)) = v;
+  };
+  if constexpr (LONG) {
+    const int imgs[2] = {0, 3};
+    stage(2, imgs);
+  } else {
+    const int imgs[4] = {0, 1, 2, 3};
+    stage(4, imgs);
   }
   __syncthreads();
   const float cs = p.scale * 1.4426950408889634f;
@@ -415,7 +438,8 @@ __global__ __launch_bounds__(AB_THREADS, 1) void attn_bwd_kernel(AttnBwdArgs p) 
       f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)   // S^T[key][q]: A = K rows, B = Q rows
-        s = mfma16x16x32(ab_row(Ks, k0 + col, kk * 4 + g), ab_row(Qs, q0 + col, kk * 4 + g), s);
+        s = mfma16x16x32(LONG ? grow(1, k0 + col, kk * 4 + g) : ab_row(Ks, k0 + col, kk * 4 + g),
+                         ab_row(Qs, q0 + col, kk * 4 + g), s);
       // lane: q = q0 + col, keys k0 + 4g + j
       float tmax = -INFINITY;
 #pragma unroll
@@ -436,7 +460,7 @@ __global__ __launch_bounds__(AB_THREADS, 1) void attn_bwd_kernel(AttnBwdArgs p) 
     }
     if (g == 0) lse[q0 + col] = (q0 + col < L) ? m + log2f(l) : INFINITY;
   }
-  for (int q = tid; q < Lp; q += AB_THREADS) {
+  for (int q = tid; q < Lp; q += NTH) {
     float d = 0.f;
     if (q < L) {
       const bf16* orow = p.o + (row0 + q) * p.ldo + h * 64;
@@ -458,6 +482,14 @@ __global__ __launch_bounds__(AB_THREADS, 1) void attn_bwd_kernel(AttnBwdArgs p) 
     f32x4 dv[4], dk[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) { dv[i] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[i] = dv[i]; }
+    bf16x8 kr[2], vr[2];   // LONG: the tile's K / V rows (B operands of every query slice)
+    if constexpr (LONG) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        kr[kk] = grow(1, k0 + col, kk * 4 + g);
+        vr[kk] = grow(2, k0 + col, kk * 4 + g);
+      }
+    }
     for (int q0 = 0; q0 < Lp; q0 += 32) {
       f32x4 s[2], dp[2];
 #pragma unroll
@@ -466,8 +498,10 @@ __global__ __launch_bounds__(AB_THREADS, 1) void attn_bwd_kernel(AttnBwdArgs p) 
         dp[hh] = s[hh];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          s[hh] = mfma16x16x32(ab_row(Qs, q0 + hh * 16 + col, kk * 4 + g), ab_row(Ks, k0 + col, kk * 4 + g), s[hh]);
-          dp[hh] = mfma16x16x32(ab_row(Os, q0 + hh * 16 + col, kk * 4 + g), ab_row(Vs, k0 + col, kk * 4 + g), dp[hh]);
+          s[hh] = mfma16x16x32(ab_row(Qs, q0 + hh * 16 + col, kk * 4 + g),
+                               LONG ? kr[kk] : ab_row(Ks, k0 + col, kk * 4 + g), s[hh]);
+          dp[hh] = mfma16x16x32(ab_row(Os, q0 + hh * 16 + col, kk * 4 + g),
+                                LONG ? vr[kk] : ab_row(Vs, k0 + col, kk * 4 + g), dp[hh]);
         }
       }
       // lane: key k0 + col, queries q0 + hh*16 + 4g + j
@@ -500,6 +534,12 @@ __global__ __launch_bounds__(AB_THREADS, 1) void attn_bwd_kernel(AttnBwdArgs p) 
       }
     }
   }
+  if constexpr (LONG) {   // Q / dO -> K / V
+    __syncthreads();
+    const int imgs[2] = {1, 2};
+    stage(2, imgs);
+    __syncthreads();
+  }
 
   // ---- pass B: dQ per 16-query tile
   for (int qt = wave; qt * 16 < L; qt += NWV) {
@@ -509,6 +549,14 @@ __global__ __launch_bounds__(AB_THREADS, 1) void attn_bwd_kernel(AttnBwdArgs p) 
     f32x4 dq[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 qr[2], orr[2];   // LONG: the query's Q / dO rows
+    if constexpr (LONG) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        qr[kk] = grow(0, q, kk * 4 + g);
+        orr[kk] = grow(3, q, kk * 4 + g);
+      }
+    }
     for (int k0 = 0; k0 < Lp; k0 += 32) {
       f32x4 s[2], dp[2];
 #pragma unroll
@@ -517,8 +565,10 @@ __global__ __launch_bounds__(AB_THREADS, 1) void attn_bwd_kernel(AttnBwdArgs p) 
         dp[hh] = s[hh];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          s[hh] = mfma16x16x32(ab_row(Ks, k0 + hh * 16 + col, kk * 4 + g), ab_row(Qs, q, kk * 4 + g), s[hh]);
-          dp[hh] = mfma16x16x32(ab_row(Vs, k0 + hh * 16 + col, kk * 4 + g), ab_row(Os, q, kk * 4 + g), dp[hh]);
+          s[hh] = mfma16x16x32(ab_row(Ks, k0 + hh * 16 + col, kk * 4 + g), LONG ? qr[kk] : ab_row(Qs, q, kk * 4 + g),
+                               s[hh]);
+          dp[hh] = mfma16x16x32(ab_row(Vs, k0 + hh * 16 + col, kk * 4 + g),
+                                LONG ? orr[kk] : ab_row(Os, q, kk * 4 + g), dp[hh]);
         }
       }
       // lane: q, keys k0 + hh*16 + 4g + j
@@ -882,7 +932,8 @@ hipError_t gelu_bwd_launch(bf16* dg, const bf16* u, long long n, hipStream_t str
 
 const char* attn_bwd_check(const AttnBwdArgs& p) {
   if (p.Dh != 64) return "attention backward: head dim 64 only";
-  if (p.L <= 0 || p.L > AB_MAXL) return "attention backward: 1 <= L <= 288 (the head's Q, K, V, dO live in LDS)";
+  if (p.L <= 0 || p.L > AB_MAXL_LONG)
+    return "attention backward: 1 <= L <= 608 (two of the head's Q, K, V, dO images live in LDS at a time)";
   if (p.B <= 0 || p.H <= 0) return "attention backward: B, H must be positive";
   if (p.ldq % 8 || p.ldo % 8 || p.lddo % 8 || p.lddq % 4) return "attention backward: row strides must be 16-byte multiples";
   return nullptr;
@@ -890,14 +941,18 @@ const char* attn_bwd_check(const AttnBwdArgs& p) {
 
 hipError_t attn_bwd_launch(const AttnBwdArgs& p, hipStream_t stream) {
   const int Lp = (p.L + 31) & ~31;
-  const int smem = 4 * Lp * 128 + 2 * Lp * 4;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               4 * AB_MAXL * 128 + 2 * AB_MAXL * 4);
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * AB_MAXL_LONG * 128 + 2 * AB_MAXL_LONG * 4);
     attr = true;
   }
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(p.B * p.H), dim3(AB_THREADS), smem, stream, p);
+  if (p.L <= AB_MAXL)
+    hipLaunchKernelGGL(attn_bwd_kernel<0>, dim3(p.B * p.H), dim3(AB_THREADS), 4 * Lp * 128 + 2 * Lp * 4, stream, p);
+  else
+    hipLaunchKernelGGL(attn_bwd_kernel<1>, dim3(p.B * p.H), dim3(AB_THREADS_LONG), 2 * Lp * 128 + 2 * Lp * 4, stream, p);
   return hipGetLastError();
 }
 

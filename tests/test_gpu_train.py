@@ -47,8 +47,11 @@ def test_wgrad_vs_torch(M, N, K, tile):
     assert rel(out3, ref) < 1e-5
 
 
-@pytest.mark.parametrize("B,L,H", [(2, 66, 1), (2, 258, 2), (3, 17, 2), (1, 288, 3), (2, 257, 1)])
+@pytest.mark.parametrize("B,L,H", [(2, 66, 1), (2, 258, 2), (3, 17, 2), (1, 288, 3), (2, 257, 1), (2, 289, 1),
+                                   (2, 334, 2), (2, 590, 2), (1, 608, 1), (3, 301, 1)])
 def test_attention_backward_vs_autograd(B, L, H):
+    """L <= 288: Q, K, V, dO resident in LDS; 288 < L <= 608 (the t2i streams: 334 image, 590 mask tokens): the
+    two-images-at-a-time kernel."""
     from panopticdiffusionmodels_amd import _lib
     Dh = 64
     g = torch.Generator().manual_seed(B * 1000 + L + H)
@@ -251,3 +254,18 @@ def test_train_label_out_of_range_raises():
     st.lr_scheduler["warmup_steps"] = 4
     out = st.train_step(torch.randn(2, 4, 16, 16, generator=g), torch.tensor([1, nc - 1]))
     assert st.step == 1 and abs(out["lr"] - st.optimizer["lr"] * 0.25) < 1e-15
+
+
+def test_attention_backward_long_repeatable():
+    """The long-sequence kernel (L = 590, the t2i mask stream) gives the same bits on every call (no atomics, fixed
+    reduction order)."""
+    from panopticdiffusionmodels_amd import _lib
+    B, L, H, Dh = 2, 590, 2, 64
+    g = torch.Generator().manual_seed(7)
+    qkv = (torch.randn(B * L, 3 * H * Dh, generator=g) * 1.5).bfloat16().to(DEV)
+    dout = torch.randn(B * L, H * Dh, generator=g).bfloat16().to(DEV)
+    o = _lib.attention(qkv, B, L, H, Dh)
+    d1 = _lib.attention_backward(qkv, o, dout, B, L, H, Dh)
+    d2 = _lib.attention_backward(qkv, o, dout, B, L, H, Dh)
+    assert torch.equal(d1, d2)
+
