@@ -329,8 +329,9 @@ int pdm_clip_encode(pdm_clip* c, const int64_t* ids, int batch, int L, float* ou
                     size_t workspace_bytes, void* stream);
 
 /* ---- training step: LSimple (sde.py:270-279, train_ldm_discrete.py:87-90) + AdamW + EMA (train_ldm_discrete.py:
- * 159-175, utils.py:308-345) of the class-conditional / unconditional U-ViT (libs/uvit.py; head dim 64, <= 288
- * tokens per image, mlp_time_embed = False) -------------------------------------------------------------------
+ * 159-175, utils.py:308-345) of the class-conditional / unconditional U-ViT (libs/uvit.py) and of the panoptic t2i
+ * U-ViT (libs/uvit_t2i.py, separate streams: train_t2i_discrete.py:148-224, 466-473); head dim 64, <= 608 tokens per
+ * stream, mlp_time_embed = False ----------------------------------------------------------------------------------
  * All parameters live in one caller-owned flat fp32 buffer; pdm_train_param_info gives each reference state_dict
  * key its element offset and count (256-B aligned, ordered head / out-blocks last..first / mid / in-blocks
  * last..first / embeddings, so each block's gradients are one contiguous range).  The caller also owns a gradient
@@ -353,6 +354,15 @@ int pdm_train_workspace_size(const pdm_trainer* t, int rows, size_t* bytes);
  * its activations in the workspace (bf16 GEMM operands, fp32 residual stream). */
 int pdm_train_step(pdm_trainer* t, const float* xt, const float* tvals, const int64_t* y, const float* target,
                    float* loss, int rows, float gscale, void* workspace, size_t workspace_bytes, void* stream);
+/* the t2i step (a trainer created from a t2i cfg): LSimple's panoptic branch with mask_token = mask_n
+ * (train_t2i_discrete.py:155-171) -- xt [rows, C, H, W] noised latent, tvals [rows] timesteps, context [rows, nctx,
+ * clip_dim] CLIP tokens, mask_token [rows, K, H, W] the noised analog bits, target the latent noise, mask_target
+ * [rows, K, H, W] the analog bits (int2bits * 2 - 1).  Writes loss[rows] = mos(target - eps_pred), loss_mask[rows] =
+ * mos(mask_pred - mask_target) and d(gscale * sum(loss + loss_mask)) / d(params) (train_t2i_discrete.py:468-473
+ * backpropagates loss_eps.mean() + loss_mask.mean()). */
+int pdm_train_step_t2i(pdm_trainer* t, const float* xt, const float* tvals, const float* context,
+                       const float* mask_token, const float* target, const float* mask_target, float* loss,
+                       float* loss_mask, int rows, float gscale, void* workspace, size_t workspace_bytes, void* stream);
 /* torch.optim.AdamW step `step` (>= 1, bias corrections 1 - beta^step) over every parameter with the gradient buffer
  * (plus grads2, same layout, when not NULL: the second lane's gradients of a batch split over two handles), then
  * ema = ema_rate * ema + (1 - ema_rate) * params (utils.ema; ema may be NULL) and the bf16 copies */
@@ -360,7 +370,7 @@ int pdm_train_adamw(pdm_trainer* t, float* m, float* v, float* ema, const float*
                     float beta2, float eps, float weight_decay, int step, float ema_rate, void* stream);
 /* the backward kernels on their own (parity tests).  pdm_wgrad: C[n][k] (+)= sum_m A[m][n] B[m][k] (bf16 A [M][lda],
  * B [M][ldb], fp32 C [N][ldc]; scratch for split-reduction partials, may be NULL).  pdm_attention_backward: softmax
- * attention over packed qkv [B*L][3*H*Dh] with output o [B*L][H*Dh] and its gradient dout -> dqkv (Dh 64, L <= 288).
+ * attention over packed qkv [B*L][3*H*Dh] with output o [B*L][H*Dh] and its gradient dout -> dqkv (Dh 64, L <= 608).
  * pdm_layernorm_backward: nn.LayerNorm(D) over fp32 rows x, dh the output gradient (fp32, or bf16 if dh_bf16) ->
  * dx (+= if accumulate), optional bf16 copy dxb, dgamma, dbeta (written); scratch >= (4 ceil(rows/4) + 1) 8 D bytes
  * is plenty. */

@@ -1,6 +1,8 @@
 """ORACLE (test infrastructure): fp32 CPU restatement of the LSimple training step.
 
-Follows train_ldm_discrete.py:54-90 (Schedule, LSimple), 159-175 (train_step), sde.py:64-69,270-279 (VPSDE sample,
+Follows train_ldm_discrete.py:54-90 (Schedule, LSimple), 159-175 (train_step), train_t2i_discrete.py:111-142,148-224,
+446-473 (the panoptic Schedule.sample, LSimple's mask branch, loss_eps.mean() + loss_mask.mean()), utils.py:475-488
+(int2bits), sde.py:64-69,270-279 (VPSDE sample,
 LSimple with ScoreModel.noise_pred: the net sees t * 999), utils.py:308-345 (torch.optim.AdamW, the 'customized'
 warm-up LambdaLR, ema).  Gradients are torch autograd through oracle/uvit_ref.uvit_forward (itself pinned to the
 reference's UViT at full size); the whole step is pinned to the reference's own training loop by
@@ -105,3 +107,43 @@ def train_steps(sd, cfg, x0, y, draws, objective, opt, warmup_steps, ema_rate):
                                            opt["weight_decay"])
             e[k] = ema(e[k], p[k], ema_rate)
     return losses, g0, p, e
+
+
+def int2bits(x, n=8):
+    """utils.int2bits (utils.py:475-488): integer masks (b, 1, h, w) -> bits (b, n, h, w), channel 0 = the most
+    significant bit (x >> (n-1)), channel n-1 = x mod 2."""
+    x = x.to(torch.int64)
+    y = torch.cat([torch.bitwise_right_shift(x, i) for i in range(n - 1, -1, -1)], dim=1)
+    return torch.remainder(y, 2).float()
+
+
+def t2i_sample(x0, scaled, np_seed, torch_seed):
+    """The t2i Schedule.sample with a panoptic mask (train_t2i_discrete.py:111-142) under np.random.seed /
+    torch.manual_seed: n ~ U{1..1000}, eps = randn_like(x0), xn; eps_m = 2 randn_like(scaled), mask_n."""
+    betas = np.append(0., sd_betas())
+    cum = (1. - betas).cumprod()
+    np.random.seed(np_seed)
+    torch.manual_seed(torch_seed)
+    n = np.random.choice(list(range(1, 1001)), (len(x0),))
+    eps = torch.randn_like(x0)
+    a = torch.from_numpy(cum[n] ** 0.5).float().view(-1, 1, 1, 1)
+    s = torch.from_numpy((1. - cum[n]) ** 0.5).float().view(-1, 1, 1, 1)
+    xn = a * x0 + s * eps
+    eps_m = 2.0 * torch.randn_like(scaled)
+    mask_n = a * scaled + s * eps_m
+    return torch.tensor(n), eps, xn, eps_m, mask_n
+
+
+def lsimple_t2i_grads(sd, cfg, xt, t_in, context, mask_n, eps, scaled):
+    """Per-sample loss_eps = mos(eps - eps_pred), loss_mask = mos(mask_pred - scaled) of the separate-stream panoptic
+    net (mask_token = mask_n) and d(loss_eps.mean() + loss_mask.mean()) / d params.  Returns (loss_eps, loss_mask,
+    grads, used): grads are zeros for parameters the forward never touches, `used` the keys that got a gradient
+    (torch.optim skips the others)."""
+    params = {k: v.detach().clone().float().requires_grad_(True) for k, v in sd.items()}
+    noise, y = uvit_ref.uvit_t2i_forward(params, cfg, xt, t_in, context, mask_token=mask_n, enable_panoptic=True)
+    le, lm = mos(eps - noise), mos(y - scaled)
+    (le.mean() + lm.mean()).backward()
+    used = {k for k, p in params.items() if p.grad is not None}
+    grads = {k: (p.grad if p.grad is not None else torch.zeros_like(p)).detach() for k, p in params.items()}
+    return le.detach(), lm.detach(), grads, used
+

@@ -174,6 +174,9 @@ _SIGS = {
     "pdm_train_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p,
                                       ctypes.c_size_t, ctypes.c_void_p]),
+    "pdm_train_step_t2i": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 8 + [ctypes.c_int, ctypes.c_float,
+                                                                                      ctypes.c_void_p, ctypes.c_size_t,
+                                                                                      ctypes.c_void_p]),
     "pdm_train_adamw": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                        ctypes.c_int, ctypes.c_float, ctypes.c_void_p]),

@@ -99,6 +99,17 @@ CONFIGS = {
         z_shape=(4, 16, 16), front_end="dpm_solver_pp", cfg_scale=1.0, decode=False,
         sample_steps=50, mini_batch_size=2, panoptic=True,
     ),
+    "tiny_t2i_train": dict(  # panoptic t2i training fixtures: Dh = 64, the full token counts (Lx 334, Lm 590), conv
+        nnet=dict(name="uvit_t2i", img_size=32, in_chans=4, patch_size=2, embed_dim=64, depth=2,
+                  num_heads=1, mlp_ratio=4, qkv_bias=False, mlp_time_embed=False, clip_dim=64,
+                  num_clip_token=77, enable_panoptic=True, use_ground_truth=False, separate=True,
+                  num_panoptic_class=8),
+        z_shape=(4, 32, 32), front_end="dpm_solver_pp", cfg_scale=1.0, decode=False,
+        sample_steps=50, mini_batch_size=2, panoptic=True,
+        train=dict(batch_size=2, objective="discrete", p_uncond=0.0, ema_rate=0.9),
+        optimizer=dict(name="adamw", lr=0.0002, weight_decay=0.03, betas=(0.99, 0.99)),
+        lr_scheduler=dict(name="customized", warmup_steps=-1),
+    ),
 }
 
 

@@ -63,9 +63,10 @@ struct AttnBwdArgs {
 const char* attn_bwd_check(const AttnBwdArgs& p);
 hipError_t attn_bwd_launch(const AttnBwdArgs& p, hipStream_t stream);
 
-// LSimple: loss[b] = mean (target - pred)^2 over `per` elements, dpred = d(gscale * sum_b loss[b]) / dpred
+// LSimple: loss[b] = mean (target - pred)^2 over `per` elements, dpred = d(gscale * sum_b loss[b]) / dpred; with
+// tanh_bwd, pred = tanh(u) and dpred is the gradient w.r.t. u (the t2i mask head's loss_mask)
 hipError_t lsimple_launch(const float* pred, const float* target, float* loss, float* dpred, int B, int per,
-                          float gscale, hipStream_t stream);
+                          float gscale, hipStream_t stream, int tanh_bwd = 0);
 
 // final_layer conv3x3 backward (NCHW fp32): din (data gradient), dw [C][C][3][3] and db [C] (written, not added)
 hipError_t conv3x3_bwd_launch(const float* dout, const float* in, const float* w, float* din, float* dw, float* db,
@@ -86,6 +87,10 @@ hipError_t patchify_launch(const float* img, bf16* pv, int B, int C, int H, int 
 // dlab[y[b]] += dx[b * L + row]
 hipError_t label_scatter_launch(const float* dx, int L, int row, int D, const int64_t* y, float* dlab, int B,
                                 hipStream_t stream);
+// dst[gd(r)] (+)= src[gs(r)], dstb[gd(r)] = bf16(dst[gd(r)]) over `rows` rows of D fp32 (D % 4 == 0); row gather
+// g(r) = (r / rpg) * gs + off + r % rpg, rpg 0 = contiguous
+hipError_t rows_add_cast_launch(float* dst, bf16* dstb, int drpg, int dgs, int doff, const float* src, int srpg, int sgs,
+                                int soff, int rows, int D, int accumulate, hipStream_t stream);
 // dx (+)= add (add may be null), dxb = bf16(dx); n % 4 == 0
 hipError_t add_cast_launch(float* dx, const float* add, bf16* dxb, long long n, hipStream_t stream);
 // W fp32 [N][K] -> W^T bf16 [K][N]

@@ -599,8 +599,9 @@ __global__ __launch_bounds__(LONG ? AB_THREADS_LONG : AB_THREADS, 1) void attn_b
 // ------------------------------------------------------------------------------------------------
 // LSimple (sde.py:270-279 / train_ldm_discrete.py:87-90): loss[b] = mean_j (target - pred)^2 (mos), and the
 // gradient of gscale * sum_b loss[b] w.r.t. pred: -2 gscale (target - pred) / per
+// tanh_bwd: pred = tanh(u) (the t2i mask head, libs/uvit_t2i.py:513) and dpred is the gradient w.r.t. u
 __global__ __launch_bounds__(256) void lsimple_kernel(const float* pred, const float* target, float* loss, float* dpred,
-                                                      int per, float gscale) {
+                                                      int per, float gscale, int tanh_bwd) {
   const int b = blockIdx.x;
   const float* pr = pred + (size_t)b * per;
   const float* tg = target + (size_t)b * per;
@@ -608,9 +609,9 @@ __global__ __launch_bounds__(256) void lsimple_kernel(const float* pred, const f
   const float k = -2.0f * gscale / (float)per;
   float s = 0.f;
   for (int i = threadIdx.x; i < per; i += 256) {
-    const float d = tg[i] - pr[i];
+    const float y = pr[i], d = tg[i] - y;
     s += d * d;
-    dp[i] = k * d;
+    dp[i] = tanh_bwd ? k * d * (1.0f - y * y) : k * d;
   }
   __shared__ float red[4];
   s = wave_sum(s);
@@ -733,6 +734,26 @@ __global__ __launch_bounds__(256) void label_scatter_kernel(const float* dx, int
 }
 
 // dx += add (fp32), dxb = bf16(dx)
+// dst[gd(r)] (+)= src[gs(r)], dstb[gd(r)] = bf16(dst[gd(r)]) over `rows` rows of D floats; g(r) = (r / rpg) * gs + off +
+// r % rpg (rpg 0: r).  The t2i mask-stream input cat(x, m): its image rows' gradient into x's, the injection's into
+// the mask output's image rows, the mask head's into the mask rows.
+__global__ __launch_bounds__(256) void rows_add_cast_kernel(float* dst, bf16* dstb, int drpg, int dgs, int doff,
+                                                            const float* src, int srpg, int sgs, int soff, int rows,
+                                                            int D, int acc) {
+  const int d4 = D >> 2;
+  const long long n = (long long)rows * d4;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const int r = (int)(e / d4), c = (int)(e % d4);
+    const size_t rd = drpg > 0 ? (size_t)(r / drpg) * dgs + doff + r % drpg : (size_t)r;
+    const size_t rs = srpg > 0 ? (size_t)(r / srpg) * sgs + soff + r % srpg : (size_t)r;
+    f32x4 v = reinterpret_cast<const f32x4*>(src + rs * D)[c];
+    f32x4* o = reinterpret_cast<f32x4*>(dst + rd * D) + c;
+    if (acc) v += *o;
+    *o = v;
+    reinterpret_cast<bf16x4*>(dstb + rd * D)[c] = to_bf16x4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 __global__ __launch_bounds__(256) void add_cast_kernel(float* dx, const float* add, bf16* dxb, long long n4) {
   for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n4; e += (long long)gridDim.x * 256) {
     f32x4 v = reinterpret_cast<f32x4*>(dx)[e];
@@ -957,8 +978,8 @@ hipError_t attn_bwd_launch(const AttnBwdArgs& p, hipStream_t stream) {
 }
 
 hipError_t lsimple_launch(const float* pred, const float* target, float* loss, float* dpred, int B, int per,
-                          float gscale, hipStream_t stream) {
-  hipLaunchKernelGGL(lsimple_kernel, dim3(B), dim3(256), 0, stream, pred, target, loss, dpred, per, gscale);
+                          float gscale, hipStream_t stream, int tanh_bwd) {
+  hipLaunchKernelGGL(lsimple_kernel, dim3(B), dim3(256), 0, stream, pred, target, loss, dpred, per, gscale, tanh_bwd);
   return hipGetLastError();
 }
 
@@ -994,6 +1015,15 @@ hipError_t label_scatter_launch(const float* dx, int L, int row, int D, const in
 hipError_t add_cast_launch(float* dx, const float* add, bf16* dxb, long long n, hipStream_t stream) {
   if (n % 4) return hipErrorInvalidValue;
   hipLaunchKernelGGL(add_cast_kernel, dim3(grid_for(n / 4)), dim3(256), 0, stream, dx, add, dxb, n / 4);
+  return hipGetLastError();
+}
+
+hipError_t rows_add_cast_launch(float* dst, bf16* dstb, int drpg, int dgs, int doff, const float* src, int srpg, int sgs,
+                                int soff, int rows, int D, int accumulate, hipStream_t stream) {
+  if (rows <= 0) return hipSuccess;
+  if (D % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rows_add_cast_kernel, dim3(grid_for((long long)rows * D / 4)), dim3(256), 0, stream, dst, dstb,
+                     drpg, dgs, doff, src, srpg, sgs, soff, rows, D, accumulate);
   return hipGetLastError();
 }
 

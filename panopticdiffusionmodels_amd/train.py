@@ -8,7 +8,10 @@ Restates, behind the reference's own names, what one training iteration does:
   * `HipTrainState.train_step` — train_ldm_discrete.py:159-175: zero_grad, loss.mean().backward(), AdamW step
     (utils.get_optimizer, torch.optim.AdamW semantics), the `customized` warm-up LR (utils.py:319-326), then the
     EMA update (utils.py:339-345, rate config.ema_rate, default 0.9999);
-  * label dropout for classifier-free guidance — datasets.py:45-61 CFGDataset (p_uncond, the null label).
+  * label dropout for classifier-free guidance — datasets.py:45-61 CFGDataset (p_uncond, the null label);
+  * the panoptic t2i step — train_t2i_discrete.py:111-142 (Schedule.sample with a mask: eps_m = 2 randn, mask_n),
+    148-224 (LSimple: analog bits utils.int2bits * 2 - 1, nnet(xn, n, context, mask_token=mask_n), loss_eps and
+    loss_mask = mos(mask_pred - bits)), 446-473 (loss_eps.mean() + loss_mask.mean() backpropagated).
 The noise draw (n / t, eps) is host-side torch RNG, as in the reference; the network forward, the loss, the whole
 backward and the optimizer run on libpdm's HIP kernels (csrc/train.hip, csrc/train_kernels.hip).  Data parallel:
 one process per GPU, the gradient buffer all-reduced (average, RCCL) between backward and optimizer step — the
@@ -41,14 +44,26 @@ class Schedule:
         self.cum_alphas = self.alphas.cumprod()
         self.cum_betas = 1. - self.cum_alphas
 
-    def sample(self, x0, rng=None):
+    def sample(self, x0, rng=None, panoptic=None):
         """(n, eps, xn), n uniform in {1..N} (np.random.choice as the reference; `rng` a numpy Generator /
-        RandomState for reproducible draws), eps ~ N(0, 1)."""
+        RandomState for reproducible draws), eps ~ N(0, 1).  With the scaled analog-bit mask `panoptic`
+        (train_t2i_discrete.py:130-142) also (eps_m, mask_n): eps_m = 2 N(0, 1), mask_n noised like xn."""
         choice = (rng or np.random).choice
         n = choice(list(range(1, self.N + 1)), (len(x0),))
         eps = torch.randn_like(x0)
         xn = stp(self.cum_alphas[n] ** 0.5, x0) + stp(self.cum_betas[n] ** 0.5, eps)
-        return torch.tensor(n, device=x0.device), eps, xn
+        if panoptic is None:
+            return torch.tensor(n, device=x0.device), eps, xn
+        eps_m = 2.0 * torch.randn_like(panoptic)
+        mask_n = stp(self.cum_alphas[n] ** 0.5, panoptic) + stp(self.cum_betas[n] ** 0.5, eps_m)
+        return torch.tensor(n, device=x0.device), eps, xn, eps_m, mask_n
+
+
+def int2bits(x, n=8):
+    """utils.int2bits (utils.py:475-488): integer masks (b, 1, h, w) -> float bits (b, n, h, w), channel 0 the most
+    significant bit."""
+    x = x.to(torch.int64)
+    return torch.remainder(torch.cat([torch.bitwise_right_shift(x, i) for i in range(n - 1, -1, -1)], 1), 2).float()
 
 
 def drop_labels(y, p_uncond, null_label, generator=None):
@@ -78,13 +93,18 @@ class HipTrainState:
         sampler lanes (sampler.py) applied to the training step."""
         _lib.require_gpu()
         kw = dict(nnet_kwargs)
-        if kw.pop("name", "uvit") != "uvit":
-            raise ValueError("HipTrainState: the class-conditional / unconditional U-ViT (libs/uvit.py) only")
+        name = kw.pop("name", "uvit")
+        if name not in ("uvit", "uvit_t2i"):
+            raise ValueError(f"HipTrainState: libs/uvit.py or libs/uvit_t2i.py networks, not {name!r}")
+        self.t2i = name == "uvit_t2i"
+        if self.t2i and lanes != 1:
+            raise ValueError("HipTrainState: the t2i step runs as one lane")
         self.kw = kw
         self.device = torch.device(device)
         self.lib = _lib.load()
         h = ctypes.c_void_p()
-        _lib.check(self.lib.pdm_train_create(ctypes.byref(cfg_struct(kw, False)), ctypes.byref(h)), "pdm_train_create")
+        _lib.check(self.lib.pdm_train_create(ctypes.byref(cfg_struct(kw, self.t2i)), ctypes.byref(h)),
+                   "pdm_train_create")
         self.h = h
         n, nwt = ctypes.c_longlong(), ctypes.c_longlong()
         _lib.check(self.lib.pdm_train_sizes(h, ctypes.byref(n), ctypes.byref(nwt)), "pdm_train_sizes")
@@ -204,11 +224,13 @@ class HipTrainState:
         t_in = t_in.to(self.device, torch.float32).contiguous().reshape(B)
         if y is not None:
             # the reference's nn.Embedding raises IndexError on an out-of-range label; the kernels would read the
-            # neighbouring parameter (pos_embed) as the embedding and scatter its gradient there, so check here
+            # neighbouring parameter (pos_embed) as the embedding and scatter its gradient there, so check here --
+            # host-side labels only (the data loader's): a check of device-resident labels would synchronise the
+            # stream every step
             nc = int(self.kw.get("num_classes", -1))
             if nc <= 0:
                 raise ValueError("HipTrainState: labels given to an unconditional U-ViT (num_classes <= 0)")
-            if y.numel():
+            if y.numel() and y.device.type == "cpu":
                 lo, hi = (int(v) for v in torch.stack([y.min(), y.max()]).cpu())
                 if lo < 0 or hi >= nc:
                     raise IndexError(f"HipTrainState: label out of range [0, {nc}): min {lo}, max {hi}")
@@ -239,6 +261,26 @@ class HipTrainState:
                 t.record_stream(s)
         return loss
 
+    def forward_backward_t2i(self, xt, t_in, context, mask_token, target, mask_target, gscale=None):
+        """The panoptic t2i step (pdm_train_step_t2i): loss[b] = mos(target - eps_pred), loss_mask[b] =
+        mos(mask_pred - mask_target) and d(gscale * sum(loss + loss_mask)) / d(params) into the gradient buffer
+        (gscale default 1/B: loss_eps.mean() + loss_mask.mean()).  Returns (loss, loss_mask)."""
+        if not self.t2i:
+            raise ValueError("forward_backward_t2i: not a t2i trainer")
+        B = xt.shape[0]
+        f32 = lambda v: v.to(self.device, torch.float32).contiguous()
+        xt, target, context, mask_token, mask_target = (f32(v) for v in (xt, target, context, mask_token, mask_target))
+        t_in = f32(t_in).reshape(B)
+        gs = float(1.0 / B if gscale is None else gscale)
+        loss = torch.empty(B, dtype=torch.float32, device=self.device)
+        loss_m = torch.empty(B, dtype=torch.float32, device=self.device)
+        ws = self._workspace(B)
+        _lib.check(self.lib.pdm_train_step_t2i(self.h, _lib.ptr(xt), _lib.ptr(t_in), _lib.ptr(context),
+                                               _lib.ptr(mask_token), _lib.ptr(target), _lib.ptr(mask_target),
+                                               _lib.ptr(loss), _lib.ptr(loss_m), B, gs, _lib.ptr(ws), ws.numel(),
+                                               _lib.stream_ptr(self.device)), "pdm_train_step_t2i")
+        return loss, loss_m
+
     def all_reduce_grads(self):
         """DDP: average the gradient buffer over the process group (RCCL on the GPU); with two lanes the second
         lane's gradients are folded in first (at world size 1 AdamW sums the two buffers itself)."""
@@ -266,9 +308,23 @@ class HipTrainState:
         """The rate the next optimizer_step applies (optimizer.param_groups[0]['lr'] after lr_scheduler.step())."""
         return customized_lr(self.optimizer["lr"], self.step, self.lr_scheduler.get("warmup_steps", -1))
 
-    def train_step(self, x0, y=None, objective="discrete", schedule=None, sde=None, rng=None):
+    def train_step(self, x0, y=None, objective="discrete", schedule=None, sde=None, rng=None, context=None,
+                   panoptic=None):
         """One iteration of train_ldm_discrete.py:159-175 (objective 'discrete', Schedule) or train_ldm.py
-        (objective 'sde', VPSDE + noise_pred).  Returns dict(loss=mean loss over the global batch, lr=...)."""
+        (objective 'sde', VPSDE + noise_pred); a t2i trainer runs train_t2i_discrete.py:446-478 on (x0, context,
+        panoptic integer masks).  Returns dict(loss=mean loss over the global batch, lr=...) (+ loss_mask)."""
+        if self.t2i:
+            schedule = schedule or Schedule(stable_diffusion_beta_schedule())
+            scaled = int2bits(panoptic).to(x0.device) * 2.0 - 1.0
+            n, eps, xn, eps_m, mask_n = schedule.sample(x0, rng, panoptic=scaled)
+            loss, loss_m = self.forward_backward_t2i(xn, n.float(), context, mask_n, eps, scaled)
+            self.all_reduce_grads()
+            self.optimizer_step()
+            ms = torch.stack([loss.mean(), loss_m.mean()])
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+                dist.all_reduce(ms, op=dist.ReduceOp.SUM)
+                ms /= dist.get_world_size()
+            return dict(loss=ms[0], loss_mask=ms[1], lr=self.current_lr())
         if objective == "discrete":
             schedule = schedule or Schedule(stable_diffusion_beta_schedule())
             n, eps, xn = schedule.sample(x0, rng)
@@ -314,4 +370,4 @@ def LSimple(x0, nnet, schedule, **kwargs):
 
 
 __all__ = ["Schedule", "stable_diffusion_beta_schedule", "LSimple", "LSimple_sde_sample", "HipTrainState",
-           "drop_labels", "customized_lr", "average_gradients"]
+           "drop_labels", "customized_lr", "average_gradients", "int2bits"]

@@ -269,3 +269,75 @@ def test_attention_backward_long_repeatable():
     d2 = _lib.attention_backward(qkv, o, dout, B, L, H, Dh)
     assert torch.equal(d1, d2)
 
+
+
+# ---- the panoptic t2i step (train_t2i_discrete.py:148-224, 446-473; libs/uvit_t2i.py separate streams) -----------
+@pytest.fixture(scope="module")
+def t2g():
+    return np.load(os.path.join(REPO, "tests", "golden", "t2i_train_golden.npz"))
+
+
+def _t2i_inputs(t2g, i):
+    return tuple(torch.from_numpy(t2g[k]) for k in (f"it{i}_xt", f"it{i}_t", "context", f"it{i}_mask_n", f"it{i}_eps",
+                                                    "scaled"))
+
+
+def test_t2i_train_step_grads_vs_reference(t2g):
+    """First iteration of the reference's t2i loop (tiny_t2i_train: the full token counts, Lx 334 / Lm 590, so both
+    attention-backward kernels' long form runs): loss_eps, loss_mask and every gradient; parameters the forward never
+    uses get none."""
+    full, kw, sd, st = _state("tiny_t2i_train")
+    loss, loss_m = st.forward_backward_t2i(*_t2i_inputs(t2g, 0))
+    assert rel(loss, t2g["it0_loss"]) < 1e-2 and rel(loss_m, t2g["it0_loss_mask"]) < 1e-2
+    grads = st.grads()
+    used = {k[5:] for k in t2g.files if k.startswith("grad/")}
+    bad = {k: rel(grads[k], t2g[f"grad/{k}"]) for k in used}
+    worst = max(bad.values())
+    assert worst < 3e-2, sorted(bad.items(), key=lambda kv: -kv[1])[:5]
+    for k in set(grads) - used:
+        assert float(grads[k].abs().max()) == 0.0, k
+
+
+def test_t2i_two_iterations_vs_reference(t2g):
+    """The reference's two-iteration t2i loop: losses and LR per iteration, the parameters' displacement; AdamW leaves
+    the unused parameters (zero_convs.{even}, mask_embed_0) exactly where they were, as torch.optim does."""
+    full, kw, sd, st = _state("tiny_t2i_train")
+    for i in range(2):
+        loss, loss_m = st.forward_backward_t2i(*_t2i_inputs(t2g, i))
+        assert rel(loss, t2g[f"it{i}_loss"]) < 1e-2 and rel(loss_m, t2g[f"it{i}_loss_mask"]) < 1e-2, i
+        lr = st.optimizer_step()
+        assert abs(lr - float(t2g[f"it{i}_lr"])) < 1e-12
+    p = st.state_dict()
+    used = {k[5:] for k in t2g.files if k.startswith("grad/")}
+    num = den = 0.0
+    for k in sd:
+        d = p[k].cpu().double() - sd[k].double()
+        if k not in used:
+            assert float(d.abs().max()) == 0.0, k
+            continue
+        d_ref = torch.from_numpy(t2g[f"delta/{k}"].astype(np.float64))
+        num += float((d - d_ref).norm() ** 2)
+        den += float(d_ref.norm() ** 2)
+    assert (num / den) ** 0.5 < 0.25, (num / den) ** 0.5
+
+
+def test_t2i_train_step_full_size_vs_oracle():
+    """MSCOCO U-ViT-S/2 t2i + panoptic mask at full width / depth / token counts (D 512, 13 blocks per stream, Lx 334,
+    Lm 590), 2 images: both losses and the gradients vs the oracle's fp32 autograd."""
+    from oracle import train_ref
+    full, kw, sd, st = _state("mscoco_uvit_small", seed=3, init="random")
+    g = torch.Generator().manual_seed(8)
+    B = 2
+    xt = torch.randn(B, 4, 32, 32, generator=g)
+    t = torch.rand(B, generator=g) * 999
+    ctx = torch.randn(B, 77, 768, generator=g)
+    scaled = train_ref.int2bits(torch.randint(0, 201, (B, 1, 32, 32), generator=g)) * 2 - 1
+    mask_n = scaled * 0.5 + torch.randn(B, 8, 32, 32, generator=g)
+    eps = torch.randn(B, 4, 32, 32, generator=g)
+    loss, loss_m = st.forward_backward_t2i(xt, t, ctx, mask_n, eps, scaled)
+    le, lm, gref, used = train_ref.lsimple_t2i_grads(sd, kw, xt, t, ctx, mask_n, eps, scaled)
+    assert rel(loss, le) < 1e-2 and rel(loss_m, lm) < 1e-2
+    grads = st.grads()
+    bad = {k: rel(grads[k], gref[k]) for k in used if float(gref[k].norm()) > 0}
+    worst = max(bad.values())
+    assert worst < 5e-2, sorted(bad.items(), key=lambda kv: -kv[1])[:5]

@@ -150,3 +150,90 @@ def _avg_worker(rank, world, port, q):
     average_gradients(g)
     q.put((rank, g.numpy()))
     dist.destroy_process_group()
+
+
+# ---- the panoptic t2i step (train_t2i_discrete.py:148-224, 446-473) ----------------------------------------------
+T2I = "tiny_t2i_train"
+
+
+@pytest.fixture(scope="module")
+def t2g():
+    return np.load(os.path.join(REPO, "tests", "golden", "t2i_train_golden.npz"))
+
+
+def _t2i_setup(t2g):
+    full = configs.get_config(T2I)
+    cfg = full["nnet"]
+    sd = weights.nnet_state_dict(cfg, seed=11, init="random")
+    kw = dict(cfg)
+    kw.pop("name")
+    x0, ctx, pan = (torch.from_numpy(t2g[k]) for k in ("x0", "context", "panoptic"))
+    return full, kw, sd, x0, ctx, pan
+
+
+def test_t2i_draws_match_reference(t2g):
+    """int2bits analog bits and the t2i Schedule.sample (n, eps, xn, mask_n) under the recorded seeds, from the oracle
+    and from the host-side train.Schedule / train.int2bits, equal the reference's draws."""
+    from panopticdiffusionmodels_amd import train
+    full, kw, sd, x0, ctx, pan = _t2i_setup(t2g)
+    scaled = train_ref.int2bits(pan) * 2.0 - 1.0
+    assert torch.equal(scaled, torch.from_numpy(t2g["scaled"]))
+    assert torch.equal(train.int2bits(pan) * 2.0 - 1.0, scaled)
+    sched = train.Schedule(train.stable_diffusion_beta_schedule())
+    for i, (nps, ts) in enumerate([(300, 400), (301, 401)]):
+        n, eps, xn, eps_m, mask_n = train_ref.t2i_sample(x0, scaled, nps, ts)
+        assert np.array_equal(n.float().numpy(), t2g[f"it{i}_t"])
+        assert np.allclose(xn.numpy(), t2g[f"it{i}_xt"], atol=1e-6)
+        assert np.allclose(mask_n.numpy(), t2g[f"it{i}_mask_n"], atol=1e-6)
+        np.random.seed(nps)
+        torch.manual_seed(ts)
+        n2, eps2, xn2, eps_m2, mask_n2 = sched.sample(x0, panoptic=scaled)
+        assert np.array_equal(n2.float().numpy(), t2g[f"it{i}_t"])
+        assert np.allclose(mask_n2.numpy(), t2g[f"it{i}_mask_n"], atol=1e-6)
+
+
+def test_t2i_oracle_loss_and_grads_vs_reference(t2g):
+    """The oracle's fp32 autograd of the separate-stream panoptic net (oracle/uvit_ref.uvit_t2i_forward) against the
+    reference's own first iteration: both losses and every used parameter's gradient; the parameters without a
+    gradient are exactly the ones the reference leaves without one."""
+    full, kw, sd, x0, ctx, pan = _t2i_setup(t2g)
+    scaled = torch.from_numpy(t2g["scaled"])
+    le, lm, g, used = train_ref.lsimple_t2i_grads(sd, kw, torch.from_numpy(t2g["it0_xt"]),
+                                                  torch.from_numpy(t2g["it0_t"]), ctx,
+                                                  torch.from_numpy(t2g["it0_mask_n"]), torch.from_numpy(t2g["it0_eps"]),
+                                                  scaled)
+    assert rel(le, t2g["it0_loss"]) < 1e-5 and rel(lm, t2g["it0_loss_mask"]) < 1e-5
+    ref_used = {k[5:] for k in t2g.files if k.startswith("grad/")}
+    assert used == ref_used
+    assert {k for k in sd if k.startswith("zero_convs.")} - used == {f"zero_convs.{i}.conv.{w}" for i in range(0, 6, 2)
+                                                                      for w in ("weight", "bias")}
+    worst = max(rel(g[k], t2g[f"grad/{k}"]) for k in used)
+    assert worst < 1e-4, worst
+
+
+def test_t2i_param_table_without_gpu():
+    """The t2i trainer's parameter table covers exactly the reference state_dict keys; the parameters the forward never
+    uses (zero_convs.{even}, mask_embed_0) come last, after every used one."""
+    from panopticdiffusionmodels_amd import _lib, native
+    lib = _lib.load()
+    for name in (T2I, "mscoco_uvit_small"):
+        kw = configs.nnet_kwargs(name)
+        kw.pop("name")
+        h = ctypes.c_void_p()
+        _lib.check(lib.pdm_train_create(ctypes.byref(native.cfg_struct(kw, True)), ctypes.byref(h)))
+        spec = {k: int(np.prod(s)) for k, s, _ in weights.uvit_t2i_spec(**kw)}
+        buf = ctypes.create_string_buffer(256)
+        seen = {}
+        for i in range(lib.pdm_train_param_count(h)):
+            off, ne = ctypes.c_longlong(), ctypes.c_longlong()
+            _lib.check(lib.pdm_train_param_info(h, i, buf, 256, ctypes.byref(off), ctypes.byref(ne)))
+            seen[buf.value.decode()] = ne.value
+        assert seen == spec, name
+        keys = list(seen)
+        unused = [k for k in keys if k.startswith("mask_embed_0.") or
+                  (k.startswith("zero_convs.") and int(k.split(".")[1]) % 2 == 0)]
+        assert keys[-len(unused):] == unused
+        ws = ctypes.c_size_t()
+        _lib.check(lib.pdm_train_workspace_size(h, 2, ctypes.byref(ws)))
+        assert ws.value > 0
+        lib.pdm_train_destroy(h)
