@@ -330,8 +330,8 @@ int pdm_clip_encode(pdm_clip* c, const int64_t* ids, int batch, int L, float* ou
 
 /* ---- training step: LSimple (sde.py:270-279, train_ldm_discrete.py:87-90) + AdamW + EMA (train_ldm_discrete.py:
  * 159-175, utils.py:308-345) of the class-conditional / unconditional U-ViT (libs/uvit.py) and of the panoptic t2i
- * U-ViT (libs/uvit_t2i.py, separate streams: train_t2i_discrete.py:148-224, 466-473); head dim 64, <= 608 tokens per
- * stream, mlp_time_embed = False ----------------------------------------------------------------------------------
+ * U-ViT (libs/uvit_t2i.py, separate streams: train_t2i_discrete.py:148-224, 466-473); head dim 64 (<= 608 tokens per
+ * stream) or 72 (U-ViT-H, <= 415), mlp_time_embed = False ----------------------------------------------------------------------------------
  * All parameters live in one caller-owned flat fp32 buffer; pdm_train_param_info gives each reference state_dict
  * key its element offset and count (256-B aligned, ordered head / out-blocks last..first / mid / in-blocks
  * last..first / embeddings, so each block's gradients are one contiguous range).  The caller also owns a gradient
@@ -370,7 +370,8 @@ int pdm_train_adamw(pdm_trainer* t, float* m, float* v, float* ema, const float*
                     float beta2, float eps, float weight_decay, int step, float ema_rate, void* stream);
 /* the backward kernels on their own (parity tests).  pdm_wgrad: C[n][k] (+)= sum_m A[m][n] B[m][k] (bf16 A [M][lda],
  * B [M][ldb], fp32 C [N][ldc]; scratch for split-reduction partials, may be NULL).  pdm_attention_backward: softmax
- * attention over packed qkv [B*L][3*H*Dh] with output o [B*L][H*Dh] and its gradient dout -> dqkv (Dh 64, L <= 608).
+ * attention over packed qkv [B*L][3*H*Dh] with output o [B*L][H*Dh] and its gradient dout -> dqkv (Dh 64, L <= 608;
+ * Dh 72, L <= 415).
  * pdm_layernorm_backward: nn.LayerNorm(D) over fp32 rows x, dh the output gradient (fp32, or bf16 if dh_bf16) ->
  * dx (+= if accumulate), optional bf16 copy dxb, dgamma, dbeta (written); scratch >= (4 ceil(rows/4) + 1) 8 D bytes
  * is plenty. */

@@ -99,6 +99,15 @@ CONFIGS = {
         z_shape=(4, 16, 16), front_end="dpm_solver_pp", cfg_scale=1.0, decode=False,
         sample_steps=50, mini_batch_size=2, panoptic=True,
     ),
+    "tiny_uvit_train_h": dict(  # training fixtures at head dim 72 (U-ViT-H): 8 heads x 72, L = 2 + 64, conv
+        nnet=dict(name="uvit", img_size=16, patch_size=2, in_chans=4, embed_dim=576, depth=2,
+                  num_heads=8, mlp_ratio=2, qkv_bias=False, mlp_time_embed=False, num_classes=11),
+        z_shape=(4, 16, 16), front_end="dpm_solver_pp", cfg_scale=0.4, decode=False,
+        sample_steps=50, mini_batch_size=2,
+        train=dict(batch_size=4, objective="discrete", p_uncond=0.15, ema_rate=0.9),
+        optimizer=dict(name="adamw", lr=0.0002, weight_decay=0.03, betas=(0.99, 0.99)),
+        lr_scheduler=dict(name="customized", warmup_steps=5),
+    ),
     "tiny_t2i_train": dict(  # panoptic t2i training fixtures: Dh = 64, the full token counts (Lx 334, Lm 590), conv
         nnet=dict(name="uvit_t2i", img_size=32, in_chans=4, patch_size=2, embed_dim=64, depth=2,
                   num_heads=1, mlp_ratio=4, qkv_bias=False, mlp_time_embed=False, clip_dim=64,

@@ -638,14 +638,15 @@ int pdm_train_create(const pdm_uvit_cfg* cfg, pdm_trainer** out) {
   if (c.t2i && !(c.separate && c.enable_panoptic))
     return pdm::set_error(PDM_ERR_ARG, "pdm_train: the t2i network trains with separate panoptic streams only");
   if (c.mlp_time_embed) return pdm::set_error(PDM_ERR_ARG, "pdm_train: mlp_time_embed is not supported");
-  if (c.embed_dim <= 0 || c.num_heads <= 0 || c.embed_dim % c.num_heads || c.embed_dim / c.num_heads != 64)
-    return pdm::set_error(PDM_ERR_ARG, "pdm_train: head dim must be 64 (the attention backward kernel)");
+  if (c.embed_dim <= 0 || c.num_heads <= 0 || c.embed_dim % c.num_heads ||
+      (c.embed_dim / c.num_heads != 64 && c.embed_dim / c.num_heads != 72))
+    return pdm::set_error(PDM_ERR_ARG, "pdm_train: head dim must be 64 or 72 (the attention backward kernel)");
   if (c.embed_dim % 64 || c.mlp_hidden % 64 || c.depth < 2)
     return pdm::set_error(PDM_ERR_ARG, "pdm_train: embed_dim / mlp hidden multiples of 64, depth >= 2");
   if (c.img_size % c.patch_size) return pdm::set_error(PDM_ERR_ARG, "pdm_train: img_size % patch_size != 0");
   pdm_trainer* t = new pdm_trainer();
   t->cfg = c;
-  t->D = c.embed_dim; t->H = c.num_heads; t->Dh = 64; t->Hid = c.mlp_hidden;
+  t->D = c.embed_dim; t->H = c.num_heads; t->Dh = c.embed_dim / c.num_heads; t->Hid = c.mlp_hidden;
   t->C = c.in_chans; t->p = c.patch_size; t->img = c.img_size;
   t->n_patch = (c.img_size / c.patch_size) * (c.img_size / c.patch_size);
   t->t2i = c.t2i != 0;
@@ -667,11 +668,11 @@ int pdm_train_create(const pdm_uvit_cfg* cfg, pdm_trainer** out) {
   t->Kpm_pad = (t->Kpm + 7) & ~7;
   t->depth = c.depth; t->nhalf = c.depth / 2; t->nb = 2 * t->nhalf + 1;   // in-blocks, mid_block, out-blocks
   const int Lmax = t->t2i ? t->Lm : t->L;
-  if (Lmax > 608 || t->P > 64 || t->P % 4 || (t->t2i && (t->PK > 64 || t->PK % 4 || t->K <= 0 || t->nctx <= 0 ||
+  if (Lmax > (t->Dh == 64 ? 608 : 415) || t->P > 64 || t->P % 4 || (t->t2i && (t->PK > 64 || t->PK % 4 || t->K <= 0 || t->nctx <= 0 ||
                                                           t->clip <= 0 || t->clip % 64))) {
     delete t;
-    return pdm::set_error(PDM_ERR_ARG, "pdm_train: tokens per stream <= 608, p*p*C (and p*p*K) <= 64 and a multiple "
-                                       "of 4, clip_dim a multiple of 64");
+    return pdm::set_error(PDM_ERR_ARG, "pdm_train: tokens per stream <= 608 (head dim 72: 415), p*p*C (and p*p*K) "
+                                       "<= 64 and a multiple of 4, clip_dim a multiple of 64");
   }
   const int D = t->D;
   auto add_block = [&](const std::string& pre, bool skip) {

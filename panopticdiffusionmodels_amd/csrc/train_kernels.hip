@@ -363,19 +363,27 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(bf16* dg, const bf16* u, 
 constexpr int AB_MAXL = 288;
 constexpr int AB_THREADS = 1024;   // one workgroup per (image, head): 16 waves over its 16-key / 16-query tiles
 
-__device__ __forceinline__ int ab_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+// a head's rows in LDS: NCHR 16-B chunks per row (8: Dh 64; 12: Dh 72 padded to 96 for the 32-deep MFMA k-steps),
+// chunks XOR-swizzled by the row within groups of 8 (and of 4 for chunks 8..11)
+template <int NCHR>
+__device__ __forceinline__ int ab_off(int row, int chunk) {
+  if constexpr (NCHR == 8) return row * 128 + ((chunk ^ (row & 7)) << 4);
+  else return row * (NCHR * 16) + ((chunk < 8 ? (chunk ^ (row & 7)) : 8 + ((chunk - 8) ^ (row & 3))) << 4);
+}
 
+template <int NCHR>
 __device__ __forceinline__ bf16x8 ab_row(const char* img, int row, int chunk) {
-  return *reinterpret_cast<const bf16x8*>(img + ab_off(row, chunk));
+  return *reinterpret_cast<const bf16x8*>(img + ab_off<NCHR>(row, chunk));
 }
 
 // A-operand fragment of X^T (rows d = d0 + (lane & 15), k-slots = the 8 image rows r0 + 4g + {0..3} and
 // r0 + 16 + 4g + {0..3}) by two transposed reads
+template <int NCHR>
 __device__ __forceinline__ bf16x8 ab_trT(const char* img, int r0, int d0, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int ra = r0 + 4 * g + q, rb = ra + 16;
   const int c = (d0 >> 3) + (p >> 1);
-  return tr_frag(img + ab_off(ra, c) + (p & 1) * 8, img + ab_off(rb, c) + (p & 1) * 8);
+  return tr_frag(img + ab_off<NCHR>(ra, c) + (p & 1) * 8, img + ab_off<NCHR>(rb, c) + (p & 1) * 8);
 }
 
 // LONG = 1 (288 < L <= 608: the t2i streams, 334 image / 590 mask tokens): the four images do not fit, so LDS holds
@@ -384,39 +392,45 @@ __device__ __forceinline__ bf16x8 ab_trT(const char* img, int r0, int d0, int la
 // arithmetic (fragments, MFMA order, P / dS rounding) is the resident kernel's, so both give the same bits where
 // both apply; 8 waves (2 per SIMD) leave room for the register-resident rows.
 constexpr int AB_MAXL_LONG = 608;
+constexpr int AB_MAXL_72 = 415;   // Dh 72: 2 x 416 rows x 192 B + lse / delta <= 160 KiB
 constexpr int AB_THREADS_LONG = 512;
 
-template <int LONG>
+// DH = 72 (U-ViT-H): rows padded to 96 (12 chunks, zeros past 72): three 32-deep k-steps for S / dP, five 16-wide
+// output tiles for dQ / dK / dV (d 72..79 of the last never stored); always the two-images-at-a-time form (L <= 415)
+template <int LONG, int DH>
 __global__ __launch_bounds__(LONG ? AB_THREADS_LONG : AB_THREADS, 1) void attn_bwd_kernel(AttnBwdArgs p) {
+  static_assert(DH == 64 || (DH == 72 && LONG), "head dims 64 / 72 (72: two images at a time)");
   constexpr int NTH = LONG ? AB_THREADS_LONG : AB_THREADS;
   constexpr int NWV = NTH / 64;   // resident: 16 waves = four per SIMD (120 VGPRs each); LONG: 8
+  constexpr int NCHR = DH == 64 ? 8 : 12, NCH = DH / 8, KK = NCHR / 4, NDT = (DH + 15) / 16, ROWB = NCHR * 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = p.L, Lp = (L + 31) & ~31;
   const int bh = blockIdx.x, b = bh / p.H, h = bh - b * p.H;
-  const int D = p.H * 64;
+  const int D = p.H * DH;
   // resident: [Q | K | V | dO]; LONG: [Q | dO], later [K | V]
   char* Qs = smem;
-  char* Ks = LONG ? smem : Qs + Lp * 128;
-  char* Vs = LONG ? smem + Lp * 128 : Ks + Lp * 128;
-  char* Os = LONG ? smem + Lp * 128 : Vs + Lp * 128;   // dO
-  float* lse = reinterpret_cast<float*>(smem + (LONG ? 2 : 4) * Lp * 128);
+  char* Ks = LONG ? smem : Qs + Lp * ROWB;
+  char* Vs = LONG ? smem + Lp * ROWB : Ks + Lp * ROWB;
+  char* Os = LONG ? smem + Lp * ROWB : Vs + Lp * ROWB;   // dO
+  float* lse = reinterpret_cast<float*>(smem + (LONG ? 2 : 4) * Lp * ROWB);
   float* dlt = lse + Lp;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t row0 = (size_t)b * L;
   // global row r (clamped to the sequence) of image img: 0 Q, 1 K, 2 V, 3 dO; 16-B chunk c
   auto grow = [&](int img, int r, int c) -> bf16x8 {
+    if (c >= NCH) return bf16x8{};   // Dh 72: the padding columns 72..95
     r = r < L ? r : L - 1;
-    const bf16* src = img < 3 ? p.qkv + (row0 + r) * p.ldq + img * D + h * 64 + c * 8
-                              : p.dout + (row0 + r) * p.lddo + h * 64 + c * 8;
+    const bf16* src = img < 3 ? p.qkv + (row0 + r) * p.ldq + img * D + h * DH + c * 8
+                              : p.dout + (row0 + r) * p.lddo + h * DH + c * 8;
     return *reinterpret_cast<const bf16x8*>(src);
   };
   // stage images (16-B chunks, rows >= L zero): slot i of LDS <- image imgs[i]
   auto stage = [&](int n, const int* imgs) {
-    for (int e = tid; e < Lp * 8 * n; e += NTH) {
-      const int i = e / (Lp * 8), r = (e / 8) % Lp, c = e & 7;
+    for (int e = tid; e < Lp * NCHR * n; e += NTH) {
+      const int i = e / (Lp * NCHR), r = (e / NCHR) % Lp, c = e % NCHR;
       bf16x8 v = bf16x8{};
       if (r < L) v = grow(imgs[i], r, c);
-      *reinterpret_cast<bf16x8*>(smem + i * Lp * 128 + ab_off(r, c)) = v;
+      *reinterpret_cast<bf16x8*>(smem + i * Lp * ROWB + ab_off<NCHR>(r, c)) = v;
     }
   };
   if constexpr (LONG) {
@@ -437,9 +451,9 @@ __global__ __launch_bounds__(LONG ? AB_THREADS_LONG : AB_THREADS, 1) void attn_b
     for (int k0 = 0; k0 < Lp; k0 += 16) {
       f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)   // S^T[key][q]: A = K rows, B = Q rows
-        s = mfma16x16x32(LONG ? grow(1, k0 + col, kk * 4 + g) : ab_row(Ks, k0 + col, kk * 4 + g),
-                         ab_row(Qs, q0 + col, kk * 4 + g), s);
+      for (int kk = 0; kk < KK; ++kk)   // S^T[key][q]: A = K rows, B = Q rows
+        s = mfma16x16x32(LONG ? grow(1, k0 + col, kk * 4 + g) : ab_row<NCHR>(Ks, k0 + col, kk * 4 + g),
+                         ab_row<NCHR>(Qs, q0 + col, kk * 4 + g), s);
       // lane: q = q0 + col, keys k0 + 4g + j
       float tmax = -INFINITY;
 #pragma unroll
@@ -463,11 +477,11 @@ __global__ __launch_bounds__(LONG ? AB_THREADS_LONG : AB_THREADS, 1) void attn_b
   for (int q = tid; q < Lp; q += NTH) {
     float d = 0.f;
     if (q < L) {
-      const bf16* orow = p.o + (row0 + q) * p.ldo + h * 64;
+      const bf16* orow = p.o + (row0 + q) * p.ldo + h * DH;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
+      for (int c = 0; c < NCH; ++c) {
         const bf16x8 ov = *reinterpret_cast<const bf16x8*>(orow + c * 8);
-        const bf16x8 dv = ab_row(Os, q, c);
+        const bf16x8 dv = ab_row<NCHR>(Os, q, c);
 #pragma unroll
         for (int j = 0; j < 8; ++j) d += (float)ov[j] * (float)dv[j];
       }
@@ -479,13 +493,13 @@ __global__ __launch_bounds__(LONG ? AB_THREADS_LONG : AB_THREADS, 1) void attn_b
   // ---- pass A: dK, dV per 16-key tile
   for (int kt = wave; kt * 16 < L; kt += NWV) {
     const int k0 = kt * 16;
-    f32x4 dv[4], dk[4];
+    f32x4 dv[NDT], dk[NDT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { dv[i] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[i] = dv[i]; }
-    bf16x8 kr[2], vr[2];   // LONG: the tile's K / V rows (B operands of every query slice)
+    for (int i = 0; i < NDT; ++i) { dv[i] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[i] = dv[i]; }
+    bf16x8 kr[KK], vr[KK];   // LONG: the tile's K / V rows (B operands of every query slice)
     if constexpr (LONG) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int kk = 0; kk < KK; ++kk) {
         kr[kk] = grow(1, k0 + col, kk * 4 + g);
         vr[kk] = grow(2, k0 + col, kk * 4 + g);
       }
@@ -497,11 +511,11 @@ __global__ __launch_bounds__(LONG ? AB_THREADS_LONG : AB_THREADS, 1) void attn_b
         s[hh] = f32x4{0.f, 0.f, 0.f, 0.f};
         dp[hh] = s[hh];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          s[hh] = mfma16x16x32(ab_row(Qs, q0 + hh * 16 + col, kk * 4 + g),
-                               LONG ? kr[kk] : ab_row(Ks, k0 + col, kk * 4 + g), s[hh]);
-          dp[hh] = mfma16x16x32(ab_row(Os, q0 + hh * 16 + col, kk * 4 + g),
-                                LONG ? vr[kk] : ab_row(Vs, k0 + col, kk * 4 + g), dp[hh]);
+        for (int kk = 0; kk < KK; ++kk) {
+          s[hh] = mfma16x16x32(ab_row<NCHR>(Qs, q0 + hh * 16 + col, kk * 4 + g),
+                               LONG ? kr[kk] : ab_row<NCHR>(Ks, k0 + col, kk * 4 + g), s[hh]);
+          dp[hh] = mfma16x16x32(ab_row<NCHR>(Os, q0 + hh * 16 + col, kk * 4 + g),
+                                LONG ? vr[kk] : ab_row<NCHR>(Vs, k0 + col, kk * 4 + g), dp[hh]);
         }
       }
       // lane: key k0 + col, queries q0 + hh*16 + 4g + j
@@ -516,18 +530,19 @@ __global__ __launch_bounds__(LONG ? AB_THREADS_LONG : AB_THREADS, 1) void attn_b
           sf[hh * 4 + j] = (bf16)(pv * (dp[hh][j] - dlt[q]));
         }
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        dv[dt] = mfma16x16x32(ab_trT(Os, q0, dt * 16, lane), pf, dv[dt]);
-        dk[dt] = mfma16x16x32(ab_trT(Qs, q0, dt * 16, lane), sf, dk[dt]);
+      for (int dt = 0; dt < NDT; ++dt) {
+        dv[dt] = mfma16x16x32(ab_trT<NCHR>(Os, q0, dt * 16, lane), pf, dv[dt]);
+        dk[dt] = mfma16x16x32(ab_trT<NCHR>(Qs, q0, dt * 16, lane), sf, dk[dt]);
       }
     }
     // lane: key k0 + col, d = dt*16 + 4g + {0..3}
     const int key = k0 + col;
     if (key < L) {
-      bf16* drow = p.dqkv + (row0 + key) * p.lddq + h * 64;
+      bf16* drow = p.dqkv + (row0 + key) * p.lddq + h * DH;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
+      for (int dt = 0; dt < NDT; ++dt) {
         const int d = dt * 16 + 4 * g;
+        if (d >= DH) break;
         *reinterpret_cast<bf16x4*>(drow + D + d) =
             to_bf16x4(dk[dt][0] * p.scale, dk[dt][1] * p.scale, dk[dt][2] * p.scale, dk[dt][3] * p.scale);
         *reinterpret_cast<bf16x4*>(drow + 2 * D + d) = to_bf16x4(dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
@@ -546,13 +561,13 @@ __global__ __launch_bounds__(LONG ? AB_THREADS_LONG : AB_THREADS, 1) void attn_b
     const int q0 = qt * 16;
     const int q = q0 + col;
     const float lq = lse[q], dq_ = dlt[q];
-    f32x4 dq[4];
+    f32x4 dq[NDT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 qr[2], orr[2];   // LONG: the query's Q / dO rows
+    for (int i = 0; i < NDT; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 qr[KK], orr[KK];   // LONG: the query's Q / dO rows
     if constexpr (LONG) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int kk = 0; kk < KK; ++kk) {
         qr[kk] = grow(0, q, kk * 4 + g);
         orr[kk] = grow(3, q, kk * 4 + g);
       }
@@ -564,11 +579,11 @@ __global__ __launch_bounds__(LONG ? AB_THREADS_LONG : AB_THREADS, 1) void attn_b
         s[hh] = f32x4{0.f, 0.f, 0.f, 0.f};
         dp[hh] = s[hh];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          s[hh] = mfma16x16x32(ab_row(Ks, k0 + hh * 16 + col, kk * 4 + g), LONG ? qr[kk] : ab_row(Qs, q, kk * 4 + g),
+        for (int kk = 0; kk < KK; ++kk) {
+          s[hh] = mfma16x16x32(ab_row<NCHR>(Ks, k0 + hh * 16 + col, kk * 4 + g), LONG ? qr[kk] : ab_row<NCHR>(Qs, q, kk * 4 + g),
                                s[hh]);
-          dp[hh] = mfma16x16x32(ab_row(Vs, k0 + hh * 16 + col, kk * 4 + g),
-                                LONG ? orr[kk] : ab_row(Os, q, kk * 4 + g), dp[hh]);
+          dp[hh] = mfma16x16x32(ab_row<NCHR>(Vs, k0 + hh * 16 + col, kk * 4 + g),
+                                LONG ? orr[kk] : ab_row<NCHR>(Os, q, kk * 4 + g), dp[hh]);
         }
       }
       // lane: q, keys k0 + hh*16 + 4g + j
@@ -582,13 +597,14 @@ __global__ __launch_bounds__(LONG ? AB_THREADS_LONG : AB_THREADS, 1) void attn_b
           sf[hh * 4 + j] = (bf16)(pv * (dp[hh][j] - dq_));
         }
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16x16x32(ab_trT(Ks, k0, dt * 16, lane), sf, dq[dt]);
+      for (int dt = 0; dt < NDT; ++dt) dq[dt] = mfma16x16x32(ab_trT<NCHR>(Ks, k0, dt * 16, lane), sf, dq[dt]);
     }
     if (q < L) {
-      bf16* drow = p.dqkv + (row0 + q) * p.lddq + h * 64;
+      bf16* drow = p.dqkv + (row0 + q) * p.lddq + h * DH;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
+      for (int dt = 0; dt < NDT; ++dt) {
         const int d = dt * 16 + 4 * g;
+        if (d >= DH) break;
         *reinterpret_cast<bf16x4*>(drow + d) =
             to_bf16x4(dq[dt][0] * p.scale, dq[dt][1] * p.scale, dq[dt][2] * p.scale, dq[dt][3] * p.scale);
       }
@@ -952,9 +968,9 @@ hipError_t gelu_bwd_launch(bf16* dg, const bf16* u, long long n, hipStream_t str
 }
 
 const char* attn_bwd_check(const AttnBwdArgs& p) {
-  if (p.Dh != 64) return "attention backward: head dim 64 only";
-  if (p.L <= 0 || p.L > AB_MAXL_LONG)
-    return "attention backward: 1 <= L <= 608 (two of the head's Q, K, V, dO images live in LDS at a time)";
+  if (p.Dh != 64 && p.Dh != 72) return "attention backward: head dim 64 or 72";
+  if (p.L <= 0 || p.L > (p.Dh == 64 ? AB_MAXL_LONG : AB_MAXL_72))
+    return "attention backward: 1 <= L <= 608 (head dim 64) / 415 (72): two of the head's Q, K, V, dO in LDS at a time";
   if (p.B <= 0 || p.H <= 0) return "attention backward: B, H must be positive";
   if (p.ldq % 8 || p.ldo % 8 || p.lddo % 8 || p.lddq % 4) return "attention backward: row strides must be 16-byte multiples";
   return nullptr;
@@ -964,16 +980,22 @@ hipError_t attn_bwd_launch(const AttnBwdArgs& p, hipStream_t stream) {
   const int Lp = (p.L + 31) & ~31;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<0, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               4 * AB_MAXL * 128 + 2 * AB_MAXL * 4);
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<1, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               2 * AB_MAXL_LONG * 128 + 2 * AB_MAXL_LONG * 4);
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<1, 72>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * 416 * 192 + 2 * 416 * 4);
     attr = true;
   }
-  if (p.L <= AB_MAXL)
-    hipLaunchKernelGGL(attn_bwd_kernel<0>, dim3(p.B * p.H), dim3(AB_THREADS), 4 * Lp * 128 + 2 * Lp * 4, stream, p);
+  if (p.Dh == 72)
+    hipLaunchKernelGGL((attn_bwd_kernel<1, 72>), dim3(p.B * p.H), dim3(AB_THREADS_LONG), 2 * Lp * 192 + 2 * Lp * 4,
+                       stream, p);
+  else if (p.L <= AB_MAXL)
+    hipLaunchKernelGGL((attn_bwd_kernel<0, 64>), dim3(p.B * p.H), dim3(AB_THREADS), 4 * Lp * 128 + 2 * Lp * 4, stream, p);
   else
-    hipLaunchKernelGGL(attn_bwd_kernel<1>, dim3(p.B * p.H), dim3(AB_THREADS_LONG), 2 * Lp * 128 + 2 * Lp * 4, stream, p);
+    hipLaunchKernelGGL((attn_bwd_kernel<1, 64>), dim3(p.B * p.H), dim3(AB_THREADS_LONG), 2 * Lp * 128 + 2 * Lp * 4,
+                       stream, p);
   return hipGetLastError();
 }
 

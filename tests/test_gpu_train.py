@@ -256,6 +256,25 @@ def test_train_label_out_of_range_raises():
     assert st.step == 1 and abs(out["lr"] - st.optimizer["lr"] * 0.25) < 1e-15
 
 
+@pytest.mark.parametrize("B,L,H", [(2, 258, 2), (1, 66, 3), (2, 17, 1), (1, 415, 1), (3, 130, 1)])
+def test_attention_backward_dh72_vs_autograd(B, L, H):
+    """Head dim 72 (U-ViT-H/2, H/4): rows padded to 96 in LDS, five 16-wide output tiles, against fp32 autograd."""
+    from panopticdiffusionmodels_amd import _lib
+    Dh = 72
+    g = torch.Generator().manual_seed(B * 100 + L + H)
+    qkv = (torch.randn(B * L, 3 * H * Dh, generator=g) * 1.5).bfloat16()
+    dout = torch.randn(B * L, H * Dh, generator=g).bfloat16()
+    q = qkv.float().reshape(B, L, 3, H, Dh).permute(2, 0, 3, 1, 4).clone().requires_grad_(True)
+    att = torch.softmax(q[0] @ q[1].transpose(-1, -2) * Dh ** -0.5, -1) @ q[2]
+    att.permute(0, 2, 1, 3).reshape(B * L, H * Dh).backward(dout.float())
+    ref = q.grad.permute(1, 3, 0, 2, 4).reshape(B * L, 3 * H * Dh)
+    o_gpu = _lib.attention(qkv.to(DEV), B, L, H, Dh)
+    dq = _lib.attention_backward(qkv.to(DEV), o_gpu, dout.to(DEV), B, L, H, Dh)
+    D = H * Dh
+    for part, sl in (("q", slice(0, D)), ("k", slice(D, 2 * D)), ("v", slice(2 * D, 3 * D))):
+        assert rel(dq[:, sl].float(), ref[:, sl]) < 1e-2, part
+
+
 def test_attention_backward_long_repeatable():
     """The long-sequence kernel (L = 590, the t2i mask stream) gives the same bits on every call (no atomics, fixed
     reduction order)."""
@@ -339,5 +358,78 @@ def test_t2i_train_step_full_size_vs_oracle():
     assert rel(loss, le) < 1e-2 and rel(loss_m, lm) < 1e-2
     grads = st.grads()
     bad = {k: rel(grads[k], gref[k]) for k in used if float(gref[k].norm()) > 0}
+    worst = max(bad.values())
+    assert worst < 5e-2, sorted(bad.items(), key=lambda kv: -kv[1])[:5]
+
+
+# ---- head dim 72 (U-ViT-H): sketches of the reference's gradients / displacements ----------------------------------
+@pytest.fixture(scope="module")
+def thg():
+    return np.load(os.path.join(REPO, "tests", "golden", "train_h_golden.npz"))
+
+
+def _sketch_rel(key, v, ref_sk, S=8):
+    """relative error of v's sketch (tests/golden/make_train_h_golden.sketch: inner products with N(0, 1) vectors seeded
+    crc32(key) + i) against the reference's"""
+    import zlib
+    v = v.detach().double().flatten().cpu()
+    sk = np.array([float(torch.randn(v.numel(), generator=torch.Generator().manual_seed(zlib.crc32(key.encode()) + i),
+                                     dtype=torch.float64) @ v) for i in range(S)])
+    return float(np.linalg.norm(sk - ref_sk[1:]) / max(np.linalg.norm(ref_sk[1:]), 1e-30))
+
+
+def test_train_h72_grads_vs_reference(thg):
+    """Head dim 72 (8 x 72, the U-ViT-H head; tiny_uvit_train_h): the reference's first-iteration loss and every
+    gradient (sketch; tensors <= 4096 elements whole)."""
+    full, kw, sd, st = _state("tiny_uvit_train_h")
+    y = torch.from_numpy(thg["y"])
+    loss = st.forward_backward(torch.from_numpy(thg["it0_xt"]), torch.from_numpy(thg["it0_t"]), y,
+                               torch.from_numpy(thg["it0_eps"]))
+    assert rel(loss, thg["it0_loss"]) < 1e-2
+    grads = st.grads()
+    bad = {k: _sketch_rel(k, grads[k], thg[f"gsk/{k}"]) for k in grads if float(thg[f"gsk/{k}"][0]) > 0}
+    worst = max(bad.values())
+    assert worst < 3e-2, sorted(bad.items(), key=lambda kv: -kv[1])[:5]
+    for k in grads:
+        if f"grad/{k}" in thg.files and float(np.linalg.norm(thg[f"grad/{k}"])) > 0:
+            assert rel(grads[k], thg[f"grad/{k}"]) < 3e-2, k
+
+
+def test_train_h72_three_iterations_vs_reference(thg):
+    """The reference's three-iteration loop at head dim 72: losses and LR per iteration, the parameters' displacement
+    (sketches, aggregated as the head-dim-64 loop test does)."""
+    full, kw, sd, st = _state("tiny_uvit_train_h")
+    y = torch.from_numpy(thg["y"])
+    for i in range(3):
+        loss = st.forward_backward(torch.from_numpy(thg[f"it{i}_xt"]), torch.from_numpy(thg[f"it{i}_t"]), y,
+                                   torch.from_numpy(thg[f"it{i}_eps"]))
+        assert rel(loss, thg[f"it{i}_loss"]) < 1e-2, i
+        lr = st.optimizer_step()
+        assert abs(lr - float(thg[f"it{i}_lr"])) < 1e-12
+    p = st.state_dict()
+    num = den = 0.0
+    for k in sd:
+        ref = thg[f"dsk/{k}"]
+        e = _sketch_rel(k, p[k].cpu().double() - sd[k].double(), ref) * np.linalg.norm(ref[1:])
+        num += e ** 2
+        den += float(np.linalg.norm(ref[1:]) ** 2)
+    assert (num / den) ** 0.5 < 0.25, (num / den) ** 0.5
+
+
+def test_train_step_full_H2_shape_vs_oracle():
+    """U-ViT-H/2 at full width / depth / token count (D 1152, 16 heads x 72, 29 blocks, L 258), 1 image: loss and
+    gradients vs the oracle's fp32 autograd."""
+    from oracle import train_ref
+    full, kw, sd, st = _state("imagenet256_uvit_huge", seed=3, init="random")
+    g = torch.Generator().manual_seed(9)
+    xt = torch.randn(1, 4, 32, 32, generator=g)
+    t = torch.rand(1, generator=g) * 999
+    y = torch.tensor([7])
+    eps = torch.randn(1, 4, 32, 32, generator=g)
+    loss = st.forward_backward(xt, t, y, eps)
+    lref, gref = train_ref.lsimple_grads(sd, kw, xt, t, y, eps)
+    assert rel(loss, lref) < 1e-2
+    grads = st.grads()
+    bad = {k: rel(grads[k], gref[k]) for k in grads if float(gref[k].norm()) > 0}
     worst = max(bad.values())
     assert worst < 5e-2, sorted(bad.items(), key=lambda kv: -kv[1])[:5]

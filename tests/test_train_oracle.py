@@ -237,3 +237,52 @@ def test_t2i_param_table_without_gpu():
         _lib.check(lib.pdm_train_workspace_size(h, 2, ctypes.byref(ws)))
         assert ws.value > 0
         lib.pdm_train_destroy(h)
+
+
+# ---- head dim 72 (U-ViT-H): sketches of the reference's gradients / displacements (tests/golden/make_train_h_golden.py)
+H72 = "tiny_uvit_train_h"
+
+
+def sketch(key, v, S=8):
+    """(norm, S projections on N(0, 1) vectors seeded crc32(key) + i) -- make_train_h_golden.sketch."""
+    import zlib
+    v = torch.as_tensor(v).detach().double().flatten().cpu()
+    pr = [float(torch.randn(v.numel(), generator=torch.Generator().manual_seed(zlib.crc32(key.encode()) + i),
+                            dtype=torch.float64) @ v) for i in range(S)]
+    return np.array([float(v.norm())] + pr)
+
+
+def sketch_rel(key, v, ref_sk):
+    sk = sketch(key, v)
+    return float(np.linalg.norm(sk[1:] - ref_sk[1:]) / max(np.linalg.norm(ref_sk[1:]), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def thg():
+    return np.load(os.path.join(REPO, "tests", "golden", "train_h_golden.npz"))
+
+
+def test_h72_oracle_vs_reference(thg):
+    """The oracle's fp32 autograd at head dim 72 against the reference's first iteration (loss, every gradient's
+    sketch, the small tensors whole) and its three-iteration loop (losses, the displacement sketches)."""
+    full = configs.get_config(H72)
+    cfg = full["nnet"]
+    sd = weights.nnet_state_dict(cfg, seed=11, init="random")
+    kw = dict(cfg)
+    kw.pop("name")
+    x0, y = torch.from_numpy(thg["x0"]), torch.from_numpy(thg["y"])
+    loss, g = train_ref.lsimple_grads(sd, kw, torch.from_numpy(thg["it0_xt"]), torch.from_numpy(thg["it0_t"]), y,
+                                      torch.from_numpy(thg["it0_eps"]))
+    assert rel(loss, thg["it0_loss"]) < 1e-5
+    worst = max(sketch_rel(k, g[k], thg[f"gsk/{k}"]) for k in sd if float(thg[f"gsk/{k}"][0]) > 0)
+    assert worst < 1e-4, worst
+    for k in sd:
+        if f"grad/{k}" in thg.files:
+            assert rel(g[k], thg[f"grad/{k}"]) < 1e-4, k
+    draws = [(100 + i, 200 + i) for i in range(3)]
+    losses, _, p, _ = train_ref.train_steps(sd, kw, x0, y, draws, "discrete", full["optimizer"],
+                                            full["lr_scheduler"]["warmup_steps"], full["train"]["ema_rate"])
+    for i in range(3):
+        assert rel(losses[i], thg[f"it{i}_loss"]) < 1e-5, i
+    worst = max(sketch_rel(k, p[k] - sd[k].float(), thg[f"dsk/{k}"]) for k in sd if float(thg[f"dsk/{k}"][0]) > 0)
+    assert worst < 1e-3, worst
