@@ -2905,10 +2905,7 @@ static hipError_t out2_copy(const GemmArgs& p, hipStream_t stream) {
                         p.stats_ld * 2, p.stats_out, p.stats_ld * 2, p.stats_out2 ? p.stats_ld * 2 : 0);
 }
 
-hipError_t gemm_launch_pair(const GemmArgs& a, const GemmArgs& b, int epi, hipStream_t stream) {
-  GemmArgs p = a, q = b;
-  p.raster = q.raster = g_gemm_raster ? g_gemm_raster : (p.N >= 8 * BN2 ? 8 : 0);
-  p.dbg_tile0 = q.dbg_tile0 = g_gemm_dbg;
+bool gemm_pair_groups(const GemmArgs& p, const GemmArgs& q, int epi) {
   const bool algo_ok = g_gemm_algo == 0 || g_gemm_algo == 11;
   const bool same = p.N == q.N && p.K == q.K && p.K1 == q.K1 && p.lda1 == q.lda1 && p.ldw == q.ldw && p.ldo == q.ldo &&
                     p.ldri == q.ldri && p.accumulate == q.accumulate && p.stats_ld == q.stats_ld && p.ln_ld == q.ln_ld &&
@@ -2916,8 +2913,14 @@ hipError_t gemm_launch_pair(const GemmArgs& a, const GemmArgs& b, int epi, hipSt
                     !p.stats_out == !q.stats_out && !p.A2 == !q.A2 && (!p.A2 || p.lda2 == q.lda2) && !p.out_fp8 && !q.out_fp8;
   // grouped only where each GEMM alone would take the persistent kernel (gemm_launch's rule), so a problem's
   // arithmetic -- and the sampler's batch invariance -- does not depend on the other problem's rows
-  if (algo_ok && same && p.M >= 4096 && q.M >= 4096 && p.N >= 256 && fits_8s(p, epi) && fits_8s(q, epi))
-    return launch8s(p, epi, stream, &q);
+  return algo_ok && same && p.M >= 4096 && q.M >= 4096 && p.N >= 256 && fits_8s(p, epi) && fits_8s(q, epi);
+}
+
+hipError_t gemm_launch_pair(const GemmArgs& a, const GemmArgs& b, int epi, hipStream_t stream) {
+  GemmArgs p = a, q = b;
+  p.raster = q.raster = g_gemm_raster ? g_gemm_raster : (p.N >= 8 * BN2 ? 8 : 0);
+  p.dbg_tile0 = q.dbg_tile0 = g_gemm_dbg;
+  if (gemm_pair_groups(p, q, epi)) return launch8s(p, epi, stream, &q);
   GemmArgs a1 = a, b1 = b;   // one flag block serves one launch
   a1.sk_flags = b1.sk_flags = nullptr;
   a1.sk_slab = b1.sk_slab = nullptr;

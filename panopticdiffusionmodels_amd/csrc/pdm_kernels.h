@@ -111,6 +111,8 @@ hipError_t rowstats_bf16_launch(const bf16* x, int ldx, int rows, int D, float* 
 
 const char* gemm_check(const GemmArgs& p, int epi);
 hipError_t gemm_launch(const GemmArgs& p, int epi, hipStream_t stream);
+// whether gemm_launch_pair runs the two problems as one grouped persistent launch (else two gemm_launch calls)
+bool gemm_pair_groups(const GemmArgs& a, const GemmArgs& b, int epi);
 // two GEMMs of the same N / K / epilogue / strides as one persistent launch when the kernel can take both (t2i image-
 // and mask-stream Linears of a layer); otherwise the two launches of gemm_launch, in order
 hipError_t gemm_launch_pair(const GemmArgs& a, const GemmArgs& b, int epi, hipStream_t stream);
