@@ -27,10 +27,20 @@ from panopticdiffusionmodels_amd.train import HipTrainState, Schedule, stable_di
 def train_flops_per_image(cfg):
     D, depth = cfg["embed_dim"], cfg["depth"]
     Hd = int(D * cfg.get("mlp_ratio", 4))
-    L = (cfg["img_size"] // cfg["patch_size"]) ** 2 + (2 if cfg.get("num_classes", -1) > 0 else 1)
+    n = (cfg["img_size"] // cfg["patch_size"]) ** 2
     nb = 2 * (depth // 2) + 1
-    gemm = nb * 2 * L * (3 * D * D + D * D + 2 * D * Hd) + (depth // 2) * 2 * L * 2 * D * D
-    attn = nb * 4 * L * L * D
+
+    def stream(L):
+        gemm = nb * 2 * L * (3 * D * D + D * D + 2 * D * Hd) + (depth // 2) * 2 * L * 2 * D * D
+        return gemm, nb * 4 * L * L * D
+
+    if cfg["name"] == "uvit_t2i":   # image stream [time, context, patches], mask stream cat(x, m), the injections
+        Lx = n + 1 + cfg.get("num_clip_token", 77)
+        gi, ai = stream(Lx)
+        gm, am = stream(Lx + n)
+        gemm, attn = gi + gm + nb * 2 * Lx * D * D, ai + am
+    else:
+        gemm, attn = stream(n + (2 if cfg.get("num_classes", -1) > 0 else 1))
     return 3 * gemm + 2.5 * attn   # fwd + dX + dW GEMMs; attention fwd + the 1.5x backward (dS, dQ/dK/dV)
 
 
@@ -48,25 +58,39 @@ def main():
     full = configs.get_config(args.config)
     dev = torch.device("cuda")
     sd = weights.nnet_state_dict(full["nnet"], seed=0, init="reference")
+    t2i = full["nnet"]["name"] == "uvit_t2i"
     st = HipTrainState(full["nnet"], dev, optimizer=full.get("optimizer"), lr_scheduler=full.get("lr_scheduler"),
-                       ema_rate=full.get("train", {}).get("ema_rate", 0.9999), lanes=args.lanes)
+                       ema_rate=full.get("train", {}).get("ema_rate", 0.9999), lanes=1 if t2i else args.lanes)
     st.load_state_dict(sd)
     del sd
     g = torch.Generator().manual_seed(0)
     B = args.batch
     x0 = torch.randn(B, *full["z_shape"], generator=g).to(dev)
     ncls = full["nnet"].get("num_classes", -1)
-    y = torch.randint(0, ncls, (B,), generator=g).to(dev) if ncls > 0 else None
+    y = torch.randint(0, ncls, (B,), generator=g).to(dev) if ncls > 0 and not t2i else None
+    if t2i:   # synthetic CLIP contexts and panoptic category masks (train_t2i_discrete.py's batch[1], batch[2])
+        from panopticdiffusionmodels_amd.train import int2bits
+        nn_ = full["nnet"]
+        ctx = torch.randn(B, nn_.get("num_clip_token", 77), nn_.get("clip_dim", 768), generator=g).to(dev)
+        pan = torch.randint(0, 201, (B, 1, nn_["img_size"], nn_["img_size"]), generator=g)
+        scaled = (int2bits(pan) * 2.0 - 1.0).to(dev)
     sched = Schedule(stable_diffusion_beta_schedule())
     import numpy as np
     rng = np.random.RandomState(0)
 
     def step(timed):
-        n, eps, xn = sched.sample(x0, rng)
         e = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed else None
-        if timed:
-            e[0].record()
-        loss = st.forward_backward(xn, n.float(), y, eps)
+        if t2i:
+            n, eps, xn, eps_m, mask_n = sched.sample(x0, rng, panoptic=scaled)
+            if timed:
+                e[0].record()
+            loss, loss_m = st.forward_backward_t2i(xn, n.float(), ctx, mask_n, eps, scaled)
+            loss = loss + loss_m
+        else:
+            n, eps, xn = sched.sample(x0, rng)
+            if timed:
+                e[0].record()
+            loss = st.forward_backward(xn, n.float(), y, eps)
         if timed:
             e[1].record()
         st.optimizer_step()
@@ -89,7 +113,8 @@ def main():
     fl = train_flops_per_image(full["nnet"])
     ips = B / dt
     print(json.dumps({
-        "metric": f"training images/s, {args.config} LSimple step (fwd + bwd + AdamW + EMA), 1 GPU",
+        "metric": f"training images/s, {args.config} LSimple step{' (panoptic: loss_eps + loss_mask)' if t2i else ''} "
+                  f"(fwd + bwd + AdamW + EMA), 1 GPU",
         "value": round(ips, 2), "unit": "images/sec", "batch": B, "steps": args.steps, "ms_per_step": round(dt * 1e3, 2),
         "fwd_bwd_ms": round(fb, 2), "adamw_ema_ms": round(opt, 2), "params": sum(v[1] for v in st.index.values()),
         "algorithmic_tflop_per_image": round(fl / 1e12, 4), "achieved_tflops": round(ips * fl / 1e12, 1),
