@@ -97,8 +97,6 @@ class HipTrainState:
         if name not in ("uvit", "uvit_t2i"):
             raise ValueError(f"HipTrainState: libs/uvit.py or libs/uvit_t2i.py networks, not {name!r}")
         self.t2i = name == "uvit_t2i"
-        if self.t2i and lanes != 1:
-            raise ValueError("HipTrainState: the t2i step runs as one lane")
         self.kw = kw
         self.device = torch.device(device)
         self.lib = _lib.load()
@@ -142,7 +140,7 @@ class HipTrainState:
         self._streams = []
         if self.lanes == 2:
             h2 = ctypes.c_void_p()
-            _lib.check(self.lib.pdm_train_create(ctypes.byref(cfg_struct(kw, False)), ctypes.byref(h2)),
+            _lib.check(self.lib.pdm_train_create(ctypes.byref(cfg_struct(kw, self.t2i)), ctypes.byref(h2)),
                        "pdm_train_create")
             self.h2 = h2
             self.G2 = torch.zeros(self.n, dtype=torch.float32, device=dev)
@@ -237,29 +235,34 @@ class HipTrainState:
             y = y.to(self.device, torch.int64).contiguous()
         gs = float(1.0 / B if gscale is None else gscale)
         loss = torch.empty(B, dtype=torch.float32, device=self.device)
+        self._lanes(B, lambda h, a, b, ws, s: self._step_call(h, xt[a:b], t_in[a:b], y[a:b] if y is not None else None,
+                                                              target[a:b], loss[a:b], gs, ws, s),
+                    (xt, t_in, target, loss) + ((y,) if y is not None else ()))
+        return loss
+
+    def _lanes(self, B, call, tensors):
+        """call(handle, row0, row1, workspace, stream) for the whole batch on the current stream, or (lanes = 2) for
+        its two halves on the lanes' own streams, joined back into the current stream."""
         cur = torch.cuda.current_stream(self.device)
         if self.lanes == 1 or B < 2:
             if self.G2 is not None:
                 self.G2.zero_()
-            self._step_call(self.h, xt, t_in, y, target, loss, gs, self._workspace(B), cur)
-            return loss
+            call(self.h, 0, B, self._workspace(B), cur)
+            return
         h0 = B // 2
-        parts = [(0, h0), (h0, B)]
         ready = torch.cuda.Event()
         ready.record(cur)
-        for lane, (a, b) in enumerate(parts):
+        for lane, (a, b) in enumerate([(0, h0), (h0, B)]):
             s = self._streams[lane]
             s.wait_event(ready)
             ws = self._workspace(b - a, lane)
             with torch.cuda.stream(s):
-                self._step_call(self.h if lane == 0 else self.h2, xt[a:b], t_in[a:b],
-                                y[a:b] if y is not None else None, target[a:b], loss[a:b], gs, ws, s)
+                call(self.h if lane == 0 else self.h2, a, b, ws, s)
             done = torch.cuda.Event()
             done.record(s)
             cur.wait_event(done)
-            for t in (xt, t_in, target, loss, ws) + ((y,) if y is not None else ()):
+            for t in tuple(tensors) + (ws,):
                 t.record_stream(s)
-        return loss
 
     def forward_backward_t2i(self, xt, t_in, context, mask_token, target, mask_target, gscale=None):
         """The panoptic t2i step (pdm_train_step_t2i): loss[b] = mos(target - eps_pred), loss_mask[b] =
@@ -274,11 +277,14 @@ class HipTrainState:
         gs = float(1.0 / B if gscale is None else gscale)
         loss = torch.empty(B, dtype=torch.float32, device=self.device)
         loss_m = torch.empty(B, dtype=torch.float32, device=self.device)
-        ws = self._workspace(B)
-        _lib.check(self.lib.pdm_train_step_t2i(self.h, _lib.ptr(xt), _lib.ptr(t_in), _lib.ptr(context),
-                                               _lib.ptr(mask_token), _lib.ptr(target), _lib.ptr(mask_target),
-                                               _lib.ptr(loss), _lib.ptr(loss_m), B, gs, _lib.ptr(ws), ws.numel(),
-                                               _lib.stream_ptr(self.device)), "pdm_train_step_t2i")
+
+        def call(h, a, b, ws, s):
+            _lib.check(self.lib.pdm_train_step_t2i(h, _lib.ptr(xt[a:b]), _lib.ptr(t_in[a:b]), _lib.ptr(context[a:b]),
+                                                   _lib.ptr(mask_token[a:b]), _lib.ptr(target[a:b]),
+                                                   _lib.ptr(mask_target[a:b]), _lib.ptr(loss[a:b]),
+                                                   _lib.ptr(loss_m[a:b]), b - a, gs, _lib.ptr(ws), ws.numel(),
+                                                   ctypes.c_void_p(s.cuda_stream)), "pdm_train_step_t2i")
+        self._lanes(B, call, (xt, t_in, context, mask_token, target, mask_target, loss, loss_m))
         return loss, loss_m
 
     def all_reduce_grads(self):

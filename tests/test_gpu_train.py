@@ -433,3 +433,30 @@ def test_train_step_full_H2_shape_vs_oracle():
     bad = {k: rel(grads[k], gref[k]) for k in grads if float(gref[k].norm()) > 0}
     worst = max(bad.values())
     assert worst < 5e-2, sorted(bad.items(), key=lambda kv: -kv[1])[:5]
+
+
+def test_t2i_train_lanes_equal_single(t2g):
+    """The t2i step on two concurrent half-batch lanes gives the single-lane losses and gradients (fp32 summation order
+    of the token reductions aside); the unused parameters stay gradient-free on both lanes."""
+    from panopticdiffusionmodels_amd import configs, weights
+    from panopticdiffusionmodels_amd.train import HipTrainState
+    full = configs.get_config("tiny_t2i_train")
+    sd = weights.nnet_state_dict(full["nnet"], seed=11, init="random")
+    sts = []
+    for lanes in (1, 2):
+        st = HipTrainState(full["nnet"], DEV, optimizer=full["optimizer"], lr_scheduler=dict(warmup_steps=-1),
+                           ema_rate=0.9, lanes=lanes)
+        st.load_state_dict(sd)
+        sts.append(st)
+    xt, t, ctx, mask_n, eps, scaled = _t2i_inputs(t2g, 0)
+    xt, t, ctx, mask_n, eps, scaled = (torch.cat([v, v.flip(0)], 0)[:3] for v in (xt, t, ctx, mask_n, eps, scaled))
+    outs = [tuple(v.cpu() for v in st.forward_backward_t2i(xt, t, ctx, mask_n, eps, scaled)) for st in sts]
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-7)
+    g1, g2 = sts[0].grads(), sts[1].grads()
+    used = {k[5:] for k in t2g.files if k.startswith("grad/")}
+    for k in g1:
+        if k in used:
+            assert rel(g2[k], g1[k]) < 1e-4 or float(g1[k].norm()) == 0, k
+        else:
+            assert float(g2[k].abs().max()) == 0.0, k

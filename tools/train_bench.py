@@ -60,7 +60,7 @@ def main():
     sd = weights.nnet_state_dict(full["nnet"], seed=0, init="reference")
     t2i = full["nnet"]["name"] == "uvit_t2i"
     st = HipTrainState(full["nnet"], dev, optimizer=full.get("optimizer"), lr_scheduler=full.get("lr_scheduler"),
-                       ema_rate=full.get("train", {}).get("ema_rate", 0.9999), lanes=1 if t2i else args.lanes)
+                       ema_rate=full.get("train", {}).get("ema_rate", 0.9999), lanes=args.lanes)
     st.load_state_dict(sd)
     del sd
     g = torch.Generator().manual_seed(0)
