@@ -563,14 +563,19 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
     // Scores live in log2 units relative to the running max: Q carries scale * log2(e) (q_log2), and every block
     // after a pass's first starts its Q K^T accumulators at -m_run, so P = exp2(S) needs no per-score FMA.
     auto do_block = [&](int c, auto tailc, auto firstc) {
-      constexpr bool TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
+      constexpr int TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
       const int kvalid = L - c * 64;
+      // TAIL 1: a ragged last block of <= 16 keys (L = 258, 334, 590): only its first 16-key sub-block is live,
+      // the others are neither computed, maxed, shifted nor exponentiated (P = 0), all decided at compile time (a
+      // runtime per-sub-block skip measured slower: the branches split the block's straight-line MFMA / VALU code).
+      // TAIL 2: any other ragged block, masked over all four sub-blocks.
+      constexpr int nkt = TAIL == 1 ? 1 : 4;
       f32x4 s[NT][4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) s[t][kt] = FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4(-m_run[t]);
-        if (TAIL && kt * 16 >= kvalid) continue;
+        if (TAIL == 1 ? kt >= 1 : (TAIL && kt * 16 >= kvalid)) continue;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbase[ks] + c * 8192 + kt * 2048);
@@ -583,7 +588,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (kt * 16 + g * 4 + j >= kvalid)
+            if (kt < nkt && kt * 16 + g * 4 + j >= kvalid)
 #pragma unroll
               for (int t = 0; t < NT; ++t) s[t][kt][j] = -INFINITY;
       }
@@ -591,14 +596,17 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
       for (int t = 0; t < NT; ++t) {
         f32x4 m4 = s[t][0];
 #pragma unroll
-        for (int kt = 1; kt < 4; ++kt)
+        for (int kt = 1; kt < 4; ++kt) {
+          if (TAIL && kt >= nkt) break;
 #pragma unroll
           for (int j = 0; j < 4; ++j) m4[j] = fmaxf(m4[j], s[t][kt][j]);
+        }
         const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
         if constexpr (FIRST) {   // the running max starts at the first block's
           m_run[t] = cmax;
 #pragma unroll
-          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= cmax;
+          for (int kt = 0; kt < 4; ++kt)
+            if (!TAIL || kt < nkt) s[t][kt] -= cmax;
         } else if (__builtin_amdgcn_ballot_w64(cmax > RESCALE_THR)) {
           // deferred rescale: the running max moves only when a block exceeds it by RESCALE_THR (rare)
           const float d = cmax > RESCALE_THR ? cmax : 0.f;
@@ -606,13 +614,18 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
           m_run[t] += d;
           l_run[t] *= alpha;
 #pragma unroll
-          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= d;
+          for (int kt = 0; kt < 4; ++kt)
+            if (!TAIL || kt < nkt) s[t][kt] -= d;
 #pragma unroll
           for (int i = 0; i < NA; ++i) acc[t][i] *= alpha;
         }
         f32x4 l4 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) {
+          if (TAIL && kt >= nkt) {
+            s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(s[t][kt][j]);
           if constexpr (!ONES) l4 += s[t][kt];
@@ -621,7 +634,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        if (TAIL && kk * 32 >= kvalid) break;
+        if (TAIL == 1 ? kk >= 1 : (TAIL && kk * 32 >= kvalid)) break;
         bf16x8 pf[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -646,7 +659,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
     if (first) block_ready(0);
     if (DEBUG != 1) {
       if (nfull > 0) do_block(0, std::false_type{}, std::true_type{});
-      else do_block(0, std::true_type{}, std::true_type{});
+      else do_block(0, std::integral_constant<int, 2>{}, std::true_type{});
     }
     for (int c = 1; c < nfull; ++c) {
       if (first) block_ready(c);
@@ -654,7 +667,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
     }
     if (nfull < nch && nfull > 0) {
       if (first) block_ready(nfull);
-      if (DEBUG != 1) do_block(nfull, std::true_type{}, std::false_type{});
+      if (DEBUG != 1) {
+        do_block(nfull, std::integral_constant<int, 2>{}, std::false_type{});
+      }
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -727,7 +742,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v2_kernel(
 // chip); here K/V traffic runs beside the MFMA / exp work of the previous head.  Every wave runs the same number of
 // passes (1-3 tiles each, balanced), so the per-block barriers of the first head's first pass and of each releasing
 // last pass pair up across waves.  Needs nqt >= NW (every wave owns a tile).  DEBUG 1: loads only; 2: math only.
-template <int DEBUG, int NW>
+// TK 1: L % 64 in [1, 16] with L > 64 (the last key block's one live sub-block resolved at compile time, do_block)
+template <int DEBUG, int NW, int TK = 2>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v3_kernel(AttentionArgs p, int nqt, int Lp) {
   constexpr int DH = 64;
   constexpr int NA = 5;                  // four PV output tiles + the ones-row tile carrying the softmax row sums
@@ -811,14 +827,19 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v3_kernel(
       for (int i = 0; i < NA; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     auto do_block = [&](int c, auto tailc, auto firstc) {
-      constexpr bool TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
+      constexpr int TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
       const int kvalid = L - c * 64;
+      // TAIL 1: a ragged last block of <= 16 keys (L = 258, 334, 590): only its first 16-key sub-block is live,
+      // the others are neither computed, maxed, shifted nor exponentiated (P = 0), all decided at compile time (a
+      // runtime per-sub-block skip measured slower: the branches split the block's straight-line MFMA / VALU code).
+      // TAIL 2: any other ragged block, masked over all four sub-blocks.
+      constexpr int nkt = TAIL == 1 ? 1 : 4;
       f32x4 s[NT][4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) s[t][kt] = FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4(-m_run[t]);
-        if (TAIL && kt * 16 >= kvalid) continue;
+        if (TAIL == 1 ? kt >= 1 : (TAIL && kt * 16 >= kvalid)) continue;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbase[ks] + c * 8192 + kt * 2048);
@@ -831,7 +852,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v3_kernel(
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (kt * 16 + g * 4 + j >= kvalid)
+            if (kt < nkt && kt * 16 + g * 4 + j >= kvalid)
 #pragma unroll
               for (int t = 0; t < NT; ++t) s[t][kt][j] = -INFINITY;
       }
@@ -839,31 +860,40 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v3_kernel(
       for (int t = 0; t < NT; ++t) {
         f32x4 m4 = s[t][0];
 #pragma unroll
-        for (int kt = 1; kt < 4; ++kt)
+        for (int kt = 1; kt < 4; ++kt) {
+          if (TAIL && kt >= nkt) break;
 #pragma unroll
           for (int j = 0; j < 4; ++j) m4[j] = fmaxf(m4[j], s[t][kt][j]);
+        }
         const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
         if constexpr (FIRST) {
           m_run[t] = cmax;
 #pragma unroll
-          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= cmax;
+          for (int kt = 0; kt < 4; ++kt)
+            if (!TAIL || kt < nkt) s[t][kt] -= cmax;
         } else if (__builtin_amdgcn_ballot_w64(cmax > RESCALE_THR)) {
           const float d = cmax > RESCALE_THR ? cmax : 0.f;
           const float alpha = __builtin_amdgcn_exp2f(-d);
           m_run[t] += d;
 #pragma unroll
-          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= d;
+          for (int kt = 0; kt < 4; ++kt)
+            if (!TAIL || kt < nkt) s[t][kt] -= d;
 #pragma unroll
           for (int i = 0; i < NA; ++i) acc[t][i] *= alpha;
         }
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+        for (int kt = 0; kt < 4; ++kt) {
+          if (TAIL && kt >= nkt) {
+            s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(s[t][kt][j]);
+        }
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        if (TAIL && kk * 32 >= kvalid) break;
+        if (TAIL == 1 ? kk >= 1 : (TAIL && kk * 32 >= kvalid)) break;
         bf16x8 pf[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -896,9 +926,11 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v3_kernel(
       }
     };
     if (nfull > 0) block(0, std::false_type{}, std::true_type{});
-    else block(0, std::true_type{}, std::true_type{});
+    else block(0, std::integral_constant<int, 2>{}, std::true_type{});
     for (int c = 1; c < nfull; ++c) block(c, std::false_type{}, std::false_type{});
-    if (nfull < nch && nfull > 0) block(nfull, std::true_type{}, std::false_type{});
+    if (nfull < nch && nfull > 0) {
+      block(nfull, std::integral_constant<int, TK>{}, std::false_type{});
+    }
     // (the next head's Q is not prefetched here by inline-asm loads: hipcc does not know such a load is in flight,
     // and across this epilogue it may hand the destination registers to other values, which the late data then
     // overwrites -- the likely cause of a GPU memory fault with that prefetch at 1600 heads, profiles/r05c)
@@ -992,7 +1024,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_v3_kernel(
 // by one asm statement took 122-126 us at 100 rows (this kernel 104) and 74-76 us at 50 rows (60): the conflict-free
 // K reads saved 2 % of the math, the 64 scattered 16-B tail reads per block cost more in the loads, so the global
 // DMA form and the 144-B rows stay here (attention_h72p_kernel, algo 14, is the persistent variant of the new layout).
-template <int DEBUG>
+template <int DEBUG, int TK = 2>   // TK: as attention_v3_kernel
 __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, int nqt, int LV, int L16) {
   constexpr int DH = 72, ROWB = 144, NCH = 9;
   constexpr float RESCALE_THR = 8.0f;
@@ -1082,12 +1114,17 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
     const char* vbase = Vs + (4 * g + (col >> 2)) * ROWB + 8 * (col & 3);
     // log2-domain scores relative to the running max, as attention_v2_kernel
     auto do_block = [&](int c, auto tailc, auto firstc) {
-      constexpr bool TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
+      constexpr int TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
       const int kvalid = L - c * 64;
+      // TAIL 1: a ragged last block of <= 16 keys (L = 258, 334, 590): only its first 16-key sub-block is live,
+      // the others are neither computed, maxed, shifted nor exponentiated (P = 0), all decided at compile time (a
+      // runtime per-sub-block skip measured slower: the branches split the block's straight-line MFMA / VALU code).
+      // TAIL 2: any other ragged block, masked over all four sub-blocks.
+      constexpr int nkt = TAIL == 1 ? 1 : 4;
       f32x4 s[NT][4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        if (TAIL && kt * 16 >= kvalid) continue;
+        if (TAIL == 1 ? kt >= 1 : (TAIL && kt * 16 >= kvalid)) continue;
         const char* krow = kbase + c * (64 * ROWB) + kt * (16 * ROWB);
         // a third 16x16x32 step over d 64..95 carries d 64..71 (k-group 0) and, in the padding slot d = 72
         // (k-group 1), K = 1 against Q = -m_run, so the chain leaves q'k - m_run with no VALU pass over the scores
@@ -1109,7 +1146,7 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (kt * 16 + g * 4 + j >= kvalid)
+            if (kt < nkt && kt * 16 + g * 4 + j >= kvalid)
 #pragma unroll
               for (int t = 0; t < NT; ++t) s[t][kt][j] = -INFINITY;
       }
@@ -1117,34 +1154,43 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
       for (int t = 0; t < NT; ++t) {
         f32x4 m4 = s[t][0];
 #pragma unroll
-        for (int kt = 1; kt < 4; ++kt)
+        for (int kt = 1; kt < 4; ++kt) {
+          if (TAIL && kt >= nkt) break;
 #pragma unroll
           for (int j = 0; j < 4; ++j) m4[j] = fmaxf(m4[j], s[t][kt][j]);
+        }
         const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
         // m_run stays bf16-representable (it enters the MFMA as a bf16 operand); the shift is exact in fp32
         if constexpr (FIRST) {
           m_run[t] = (float)(bf16)cmax;
 #pragma unroll
-          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= m_run[t];
+          for (int kt = 0; kt < 4; ++kt)
+            if (!TAIL || kt < nkt) s[t][kt] -= m_run[t];
           set_qm(t);
         } else if (__builtin_amdgcn_ballot_w64(cmax > RESCALE_THR)) {
           const float d = cmax > RESCALE_THR ? (float)(bf16)(m_run[t] + cmax) - m_run[t] : 0.f;
           const float alpha = __builtin_amdgcn_exp2f(-d);
           m_run[t] += d;
 #pragma unroll
-          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= d;
+          for (int kt = 0; kt < 4; ++kt)
+            if (!TAIL || kt < nkt) s[t][kt] -= d;
 #pragma unroll
           for (int i = 0; i < 5; ++i) acc[t][i] *= alpha;
           set_qm(t);
         }
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+        for (int kt = 0; kt < 4; ++kt) {
+          if (TAIL && kt >= nkt) {
+            s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(s[t][kt][j]);
+        }
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        if (TAIL && kk * 32 >= kvalid) break;
+        if (TAIL == 1 ? kk >= 1 : (TAIL && kk * 32 >= kvalid)) break;
         bf16x8 pf[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -1170,7 +1216,7 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
     if (first) block_ready(0);
     if (DEBUG != 1) {
       if (nfull > 0) do_block(0, std::false_type{}, std::true_type{});
-      else do_block(0, std::true_type{}, std::true_type{});
+      else do_block(0, std::integral_constant<int, 2>{}, std::true_type{});
     }
     for (int c = 1; c < nfull; ++c) {
       if (first) block_ready(c);
@@ -1178,7 +1224,9 @@ __global__ __launch_bounds__(256, 2) void attention_h72_kernel(AttentionArgs p, 
     }
     if (nfull < nch && nfull > 0) {
       if (first) block_ready(nfull);
-      if (DEBUG != 1) do_block(nfull, std::true_type{}, std::false_type{});
+      if (DEBUG != 1) {
+        do_block(nfull, std::integral_constant<int, TK>{}, std::false_type{});
+      }
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -1362,12 +1410,17 @@ __global__ __launch_bounds__(256, 2) void attention_h72p_kernel(AttentionArgs p,
       for (int i = 0; i < 5; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     auto do_block = [&](int c, auto tailc, auto firstc) {
-      constexpr bool TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
+      constexpr int TAIL = decltype(tailc)::value, FIRST = decltype(firstc)::value;
       const int kvalid = L - c * 64;
+      // TAIL 1: a ragged last block of <= 16 keys (L = 258, 334, 590): only its first 16-key sub-block is live,
+      // the others are neither computed, maxed, shifted nor exponentiated (P = 0), all decided at compile time (a
+      // runtime per-sub-block skip measured slower: the branches split the block's straight-line MFMA / VALU code).
+      // TAIL 2: any other ragged block, masked over all four sub-blocks.
+      constexpr int nkt = TAIL == 1 ? 1 : 4;
       f32x4 s[NT][4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        if (TAIL && kt * 16 >= kvalid) continue;
+        if (TAIL == 1 ? kt >= 1 : (TAIL && kt * 16 >= kvalid)) continue;
         bf16x8 kx = *reinterpret_cast<const bf16x8*>(ktail + c * 1024 + kt * 256);
         kx = g == 0 ? kx : (g == 1 ? one8 : zero8);
 #pragma unroll
@@ -1384,7 +1437,7 @@ __global__ __launch_bounds__(256, 2) void attention_h72p_kernel(AttentionArgs p,
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (kt * 16 + g * 4 + j >= kvalid)
+            if (kt < nkt && kt * 16 + g * 4 + j >= kvalid)
 #pragma unroll
               for (int t = 0; t < NT; ++t) s[t][kt][j] = -INFINITY;
       }
@@ -1392,33 +1445,42 @@ __global__ __launch_bounds__(256, 2) void attention_h72p_kernel(AttentionArgs p,
       for (int t = 0; t < NT; ++t) {
         f32x4 m4 = s[t][0];
 #pragma unroll
-        for (int kt = 1; kt < 4; ++kt)
+        for (int kt = 1; kt < 4; ++kt) {
+          if (TAIL && kt >= nkt) break;
 #pragma unroll
           for (int j = 0; j < 4; ++j) m4[j] = fmaxf(m4[j], s[t][kt][j]);
+        }
         const float cmax = xrow_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
         if constexpr (FIRST) {
           m_run[t] = (float)(bf16)cmax;
 #pragma unroll
-          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= m_run[t];
+          for (int kt = 0; kt < 4; ++kt)
+            if (!TAIL || kt < nkt) s[t][kt] -= m_run[t];
           set_qm(t);
         } else if (__builtin_amdgcn_ballot_w64(cmax > RESCALE_THR)) {
           const float d = cmax > RESCALE_THR ? (float)(bf16)(m_run[t] + cmax) - m_run[t] : 0.f;
           const float alpha = __builtin_amdgcn_exp2f(-d);
           m_run[t] += d;
 #pragma unroll
-          for (int kt = 0; kt < 4; ++kt) s[t][kt] -= d;
+          for (int kt = 0; kt < 4; ++kt)
+            if (!TAIL || kt < nkt) s[t][kt] -= d;
 #pragma unroll
           for (int i = 0; i < 5; ++i) acc[t][i] *= alpha;
           set_qm(t);
         }
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+        for (int kt = 0; kt < 4; ++kt) {
+          if (TAIL && kt >= nkt) {
+            s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) s[t][kt][j] = __builtin_amdgcn_exp2f(s[t][kt][j]);
+        }
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        if (TAIL && kk * 32 >= kvalid) break;
+        if (TAIL == 1 ? kk >= 1 : (TAIL && kk * 32 >= kvalid)) break;
         bf16x8 pf[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -1449,9 +1511,11 @@ __global__ __launch_bounds__(256, 2) void attention_h72p_kernel(AttentionArgs p,
       }
     };
     if (nfull > 0) block(0, std::false_type{}, std::true_type{});
-    else block(0, std::true_type{}, std::true_type{});
+    else block(0, std::integral_constant<int, 2>{}, std::true_type{});
     for (int c = 1; c < nfull; ++c) block(c, std::false_type{}, std::false_type{});
-    if (nfull < nch && nfull > 0) block(nfull, std::true_type{}, std::false_type{});
+    if (nfull < nch && nfull > 0) {
+      block(nfull, std::integral_constant<int, 2>{}, std::false_type{});
+    }
     // (no prefetch of the next head's Q here as in attention_v3_kernel: held across the passes it spills at NT = 3)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -1542,6 +1606,8 @@ const char* attention_check(const AttentionArgs& p) {
   return nullptr;
 }
 
+// the last key block holds 1..16 keys behind >= 1 full block (L = 258, 334, 590): the kernels' TK = 1 tail
+static bool tail1(int L) { return L > 64 && L % 64 != 0 && L % 64 <= 16; }
 static int g_attention_algo = 0;   // 0 auto, 1 streamed K/V, 2/3 head-resident T = 2/3, 4 head-resident v2 (5/6 timing)
 void attention_set_algo(int algo) { g_attention_algo = algo; }
 
@@ -1579,6 +1645,7 @@ hipError_t attention_launch(const AttentionArgs& args, hipStream_t stream) {
     static bool attr72 = false;
     if (!attr72) {
       (void)hipFuncSetAttribute((const void*)attention_h72_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)attention_h72_kernel<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
       (void)hipFuncSetAttribute((const void*)attention_h72_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
       (void)hipFuncSetAttribute((const void*)attention_h72_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
       attr72 = true;
@@ -1586,6 +1653,7 @@ hipError_t attention_launch(const AttentionArgs& args, hipStream_t stream) {
     const dim3 grid(p.B * p.H), block(256);
     if (algo == 8) hipLaunchKernelGGL(attention_h72_kernel<1>, grid, block, smem72, stream, p, nqt, LV, L16);
     else if (algo == 9) hipLaunchKernelGGL(attention_h72_kernel<2>, grid, block, smem72, stream, p, nqt, LV, L16);
+    else if (tail1(p.L)) hipLaunchKernelGGL((attention_h72_kernel<0, 1>), grid, block, smem72, stream, p, nqt, LV, L16);
     else hipLaunchKernelGGL(attention_h72_kernel<0>, grid, block, smem72, stream, p, nqt, LV, L16);
     return hipGetLastError();
   }
@@ -1601,9 +1669,11 @@ hipError_t attention_launch(const AttentionArgs& args, hipStream_t stream) {
       static int ncu = 256;
       if (!attr3) {
         (void)hipFuncSetAttribute((const void*)attention_v3_kernel<0, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)attention_v3_kernel<0, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)attention_v3_kernel<1, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)attention_v3_kernel<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)attention_v3_kernel<0, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)attention_v3_kernel<0, 8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)attention_v3_kernel<1, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)attention_v3_kernel<2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         int dev = 0, n = 0;
@@ -1614,11 +1684,13 @@ hipError_t attention_launch(const AttentionArgs& args, hipStream_t stream) {
       const int nbh = p.B * p.H, slots = ncu * (nw == 4 ? 2 : 1);
       const dim3 grid(nbh < slots ? nbh : slots);
       if (nw == 4) {
-        if (algo == 11) hipLaunchKernelGGL((attention_v3_kernel<0, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
+        if (algo == 11 && tail1(p.L)) hipLaunchKernelGGL((attention_v3_kernel<0, 4, 1>), grid, dim3(256), smem, stream, p, nqt, Lp);
+        else if (algo == 11) hipLaunchKernelGGL((attention_v3_kernel<0, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
         else if (algo == 12) hipLaunchKernelGGL((attention_v3_kernel<1, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
         else hipLaunchKernelGGL((attention_v3_kernel<2, 4>), grid, dim3(256), smem, stream, p, nqt, Lp);
       } else {
-        if (algo == 11) hipLaunchKernelGGL((attention_v3_kernel<0, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
+        if (algo == 11 && tail1(p.L)) hipLaunchKernelGGL((attention_v3_kernel<0, 8, 1>), grid, dim3(512), smem, stream, p, nqt, Lp);
+        else if (algo == 11) hipLaunchKernelGGL((attention_v3_kernel<0, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
         else if (algo == 12) hipLaunchKernelGGL((attention_v3_kernel<1, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
         else hipLaunchKernelGGL((attention_v3_kernel<2, 8>), grid, dim3(512), smem, stream, p, nqt, Lp);
       }
