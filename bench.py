@@ -60,6 +60,7 @@ def parse():
                     help="sample the batch as this many concurrent sub-batches on their own streams (fills the "
                          "partly idle last GEMM wave of batches whose rows tile the 256-row GEMM unevenly)")
     ap.add_argument("--no-decode", action="store_true")
+    ap.add_argument("--decode-lanes", type=int, default=2, help="concurrent decode chunks (libs/autoencoder.py)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--precision", choices=["bf16", "fp8", "fp8-all"], default=None,
@@ -132,7 +133,8 @@ def main():
                                    use_graph=not args.no_graph, lanes=args.lanes)
     # configs[0] (CIFAR-10) samples pixels: no autoencoder (eval.py:56-86)
     decode = full.get("decode", True) and not args.no_decode
-    ae = get_model(None, scale_factor=full.get("scale_factor", 0.18215), seed=1).to(dev) if decode else None
+    ae = get_model(None, scale_factor=full.get("scale_factor", 0.18215), seed=1,
+                   lanes=args.decode_lanes).to(dev) if decode else None
 
     # inputs for every (warmup + timed) step, generated per GLOBAL sample index and resident in HBM
     nsteps = args.warmup + args.steps

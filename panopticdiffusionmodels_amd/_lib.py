@@ -224,6 +224,27 @@ def check(status, what=""):
         raise RuntimeError(f"{what}: {msg}" if what else msg)
 
 
+# Priority of the lane streams.  HIP keeps one pool of hardware queues per stream priority, each capped at
+# GPU_MAX_HW_QUEUES (4 by default): a normal-priority lane stream shares a queue with the caller's stream or RCCL's
+# once the process has made a few streams (torchrun / accelerate), and the lanes then run one after the other.
+LANE_STREAM_PRIORITY = int(os.environ.get("PDM_LANE_PRIORITY", "-1"))
+_LANE_STREAMS = {}
+
+
+def lane_streams(device, n):
+    """The process's n side streams on `device` (LANE_STREAM_PRIORITY), shared by every multi-lane user (the
+    samplers' lanes, the decoder's lanes): each extra stream a process makes can take a hardware queue the sampling
+    lanes need (two decoder streams of their own cost the L/2 bench 55-60 ms of sampling per step), so lanes reuse
+    these few instead of making their own.  Users run one after the other from one host thread and order their lanes
+    against the caller's stream on entry and exit."""
+    dev = torch.device(device)
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    pool = _LANE_STREAMS.setdefault(key, [])
+    while len(pool) < n:
+        pool.append(torch.cuda.Stream(device=dev, priority=LANE_STREAM_PRIORITY))
+    return pool[:n]
+
+
 def require_gpu(t=None):
     if not torch.cuda.is_available():
         raise RuntimeError("panopticdiffusionmodels_amd runs on an MI355X (gfx950) GPU; no GPU is visible "

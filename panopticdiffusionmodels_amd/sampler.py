@@ -11,7 +11,6 @@ each a separate PyTorch launch, plus host syncs inside the discrete schedule.  H
 with every coefficient precomputed on the host (solver_core).  Nothing in the loop synchronises with the
 host, so the 50-NFE loop for a fixed batch is captured once into a HIP graph and replayed.
 """
-import os
 
 import torch
 
@@ -58,18 +57,11 @@ def _drop_stale_graph(st, nnet):
         st["generation"] = nnet.generation
 
 
-# Priority of the lanes' own streams.  HIP keeps one pool of hardware queues per stream priority, each capped at
-# GPU_MAX_HW_QUEUES (4 by default): a normal-priority lane stream shares a queue with the caller's stream or RCCL's
-# once the process has made a few streams (torchrun / accelerate), and the lanes then run one after the other.
-LANE_STREAM_PRIORITY = int(os.environ.get("PDM_LANE_PRIORITY", "-1"))
-
-
 def _lane_streams(owner, main):
-    """Streams of the concurrent lanes: lane 0 runs on the caller's stream, lanes 1.. on streams of their own
-    (LANE_STREAM_PRIORITY), so a lane never waits behind another lane's kernels in a shared hardware queue."""
-    while len(owner._streams) < owner.lanes - 1:
-        owner._streams.append(torch.cuda.Stream(device=main.device, priority=LANE_STREAM_PRIORITY))
-    return [main] + owner._streams[:owner.lanes - 1]
+    """Streams of the concurrent lanes: lane 0 runs on the caller's stream, lanes 1.. on the process's shared side
+    streams (_lib.lane_streams: high priority, so a lane never waits behind another lane's kernels in a shared
+    hardware queue)."""
+    return [main] + _lib.lane_streams(main.device, owner.lanes - 1)
 
 
 class ClassCondSampler:
@@ -91,7 +83,6 @@ class ClassCondSampler:
         # streams, each with a private workspace and graph, so one lane's GEMMs fill the CUs the other's leave
         # idle in a partly filled last wave (batches whose 2B * L rows tile the 256-row GEMM unevenly)
         self.lanes = max(1, int(lanes))
-        self._streams = []
         self._state = {}
         self.nfe = sc.nfe(self.plan)
 
@@ -210,7 +201,6 @@ class T2ISampler:
     def __init__(self, nnet, cfg_scale=1.0, steps=50, betas=None, enable_mask_opt=True, use_graph=True, lanes=1):
         self.nnet = nnet
         self.lanes = max(1, int(lanes))   # concurrent sub-batches (ClassCondSampler)
-        self._streams = []
         hs = sc.HostDiscrete(betas=sd_betas() if betas is None else betas)
         self.plan = sc.pp_fast_plan(hs, steps, 1.0 / hs.N, 1.0, order=3, predict_x0=True,
                                     enable_mask_opt=enable_mask_opt)

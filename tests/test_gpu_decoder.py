@@ -59,6 +59,20 @@ def test_decoder_chunked_batch_vs_oracle(dev):
     assert rel(alone, img[2:3]) < 1e-5
 
 
+def test_decoder_two_lanes_bit_identical(dev):
+    """B = 5 in balanced chunks of <= 2 (2 + 2 + 1) decoded on two concurrent streams (the default) equals the
+    one-stream decode bit for bit, and the caller's stream sees the finished images."""
+    ae, _ = _ae(64, (1, 2), 1, 9, "random", 16, chunk=2)
+    ae = ae.to(dev)
+    g = torch.Generator().manual_seed(9)
+    z = torch.randn(5, 4, 16, 16, generator=g).to(dev)
+    two = ae.decode(z).clone()
+    ae.lanes = 1
+    one = ae.decode(z)
+    assert torch.equal(two, one)
+    assert torch.isfinite(one).all()
+
+
 def test_decoder_latent64_vs_oracle(dev):
     """512x512 decode (latent 64, BASELINE configs[4]) of two images in one chunk: 4096-token mid attention,
     512^2 output, every image vs the oracle."""
