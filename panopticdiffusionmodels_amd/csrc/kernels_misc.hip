@@ -394,20 +394,23 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* x, bf16* y,
 }
 
 // ------------------------------------------------------------------------------------------------
-// MXFP8 quantisation of rows (pdm_mx_quantize; in the fp8 forward: attention output -> attn.proj operand).
-// One thread per 8 consecutive columns, so the 4 consecutive lanes of a 32-column block reduce its amax with
-// two xor-shuffles (mx_quant8: the quantiser of the MXFP8-emitting GEMM epilogues, bit for bit).
+// MXFP8 quantisation of rows (pdm_mx_quantize; in the fp8 forward: attention output -> attn.proj operand), tiled as
+// 16 rows x 128 columns per block, 16 lanes per row with 8 consecutive columns each: the 4 lanes of a 32-column block
+// reduce its amax with two xor-shuffles (mx_quant8: the quantiser of the MXFP8-emitting GEMM epilogues, bit for bit),
+// then a row's four E8M0 bytes of its 128-column group are gathered into its first lane and stored as ONE dword -- the
+// 16 rows' dwords of a group are consecutive in the [K/128][s_ld] scale layout.  (Round 4's one-thread-per-8-columns
+// form stored one scattered byte per 32-column block: 15.0 us per H/4 call at 50 rows.)  Blocks past K get scale byte
+// 0, the zero padding of a partial last group.
 template <typename T>
-__global__ __launch_bounds__(256) void mxq_kernel(const T* x, int ldx, int rows, int K, unsigned char* q, int ldq,
-                                                  unsigned* s, int s_ld) {
-  const int nch = K >> 3;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  const bool ok = i < (long long)rows * nch;
-  const int r = ok ? (int)(i / nch) : 0;
-  const int c = ok ? (int)(i - (long long)r * nch) : 0;
+__global__ __launch_bounds__(256) void mxq_tiled_kernel(const T* x, int ldx, int rows, int K, unsigned char* q,
+                                                        int ldq, unsigned* s, int s_ld) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int c = blockIdx.y * 128 + (threadIdx.x & 15) * 8;
+  const bool ok = r < rows && c < K;
   float f[8];
   if (ok) {
-    const T* p = x + (size_t)r * ldx + c * 8;
+    const T* p = x + (size_t)r * ldx + c;
     if constexpr (sizeof(T) == 4) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
 #pragma unroll
@@ -422,8 +425,17 @@ __global__ __launch_bounds__(256) void mxq_kernel(const T* x, int ldx, int rows,
     for (int j = 0; j < 8; ++j) f[j] = 0.f;
   }
   unsigned e8;
-  const uint2 w = mx_quant8(f, &e8);   // every lane joins the block shuffles (K % 32 == 0: blocks never straddle rows)
-  if (ok) mx_store8(q, ldq, s, s_ld, r, c * 8, w, e8, (c & 3) == 0);
+  const uint2 w = mx_quant8(f, &e8);
+  if (ok) *reinterpret_cast<uint2*>(q + (size_t)r * ldq + c) = w;
+  const int base = lane & ~15;
+  const int g0 = blockIdx.y * 128;
+  unsigned dw = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const unsigned eb = (unsigned)__shfl((int)e8, base + 4 * b, 64);
+    dw |= (g0 + 32 * b < K ? eb : 0u) << (8 * b);
+  }
+  if ((threadIdx.x & 15) == 0 && r < rows) s[(size_t)blockIdx.y * s_ld + r] = dw;
 }
 
 inline int grid_for(long long n) {
@@ -548,10 +560,9 @@ hipError_t mxq_launch(const void* x, int dtype, int ldx, int rows, int K, unsign
       (dtype != 0 && dtype != 1) || (f32 ? ldx % 4 : ldx % 8) || ((uintptr_t)x & 15) || ((uintptr_t)q & 7) ||
       ((uintptr_t)s & 3))
     return hipErrorInvalidValue;
-  const long long n = (long long)rows * (K >> 3);
-  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-  if (f32) hipLaunchKernelGGL(mxq_kernel<float>, grid, block, 0, stream, (const float*)x, ldx, rows, K, q, ldq, s, s_ld);
-  else hipLaunchKernelGGL(mxq_kernel<bf16>, grid, block, 0, stream, (const bf16*)x, ldx, rows, K, q, ldq, s, s_ld);
+  const dim3 grid((unsigned)((rows + 15) / 16), (unsigned)((K + 127) / 128)), block(256);
+  if (f32) hipLaunchKernelGGL(mxq_tiled_kernel<float>, grid, block, 0, stream, (const float*)x, ldx, rows, K, q, ldq, s, s_ld);
+  else hipLaunchKernelGGL(mxq_tiled_kernel<bf16>, grid, block, 0, stream, (const bf16*)x, ldx, rows, K, q, ldq, s, s_ld);
   return hipGetLastError();
 }
 

@@ -203,7 +203,7 @@ def test_mx_center_argument_checks(lib):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("R,K", [(1, 32), (77, 1152), (2581, 1152), (300, 4608)])
+@pytest.mark.parametrize("R,K", [(1, 32), (17, 96), (77, 1152), (2581, 1152), (300, 4608)])
 def test_mx_quantize_kernel_bit_exact(lib, dtype, R, K):
     """pdm_mx_quantize (attention output -> proj operand in the fp8 forward) == the host quantiser, bit for bit,
     including blocks of very different magnitude and all-zero blocks."""
