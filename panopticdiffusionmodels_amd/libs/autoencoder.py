@@ -14,7 +14,7 @@ decode_large_batch in eval_ldm_discrete.py:62-68) so the workspace stays bounded
 25 + 25, not 32 + 18) and alternate over `lanes` streams -- the caller's and the process's shared lane streams
 (_lib.lane_streams, the sampler's) -- with a workspace each, so two chunks decode at once and one's small
 low-resolution launches fill the CUs the other leaves idle (B = 50: 47.3 -> 45.1 ms at 256^2, 183.0 -> 179.8 ms at
-512^2, bit-identical; tools/decode_lanes.py).
+512^2; B = 32, split 16 + 16: 29.1 -> 28.3 ms, 116.4 -> 113.6 ms; bit-identical; tools/decode_lanes.py).
 """
 import ctypes
 
@@ -171,7 +171,8 @@ class FrozenAutoencoderKL(nn.Module):
         z = z.float().contiguous()
         up = 2 ** (len(self.ch_mult) - 1)
         img = torch.empty(B, self.out_ch, h * up, w * up, dtype=torch.float32, device=z.device)
-        nch = -(-B // self.chunk)
+        # at least one chunk per lane once each gets >= 8 latents (B = 32: 16 + 16 concurrently, 29.1 -> 28.3 ms at 256^2)
+        nch = max(-(-B // self.chunk), min(self.lanes, B // 8))
         sizes = [B // nch + (1 if i < B % nch else 0) for i in range(nch)]   # balanced chunks of <= chunk
         starts = [sum(sizes[:i]) for i in range(nch)]
         lanes = min(self.lanes, nch)
