@@ -22,6 +22,15 @@ namespace pdm {
 
 namespace {
 constexpr int BM = 128, BN = 128, BK = 64;
+
+template <int... I, class F>
+__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  sfor_impl(std::make_integer_sequence<int, N>{}, f);
+}
 // bf16 / GELU epilogues: one bf16 output row per stored row, bias and the fused-LayerNorm consumer apply
 constexpr bool epi_rowout(int e) { return e == EPI_BF16 || e == EPI_GELU; }
 
@@ -1251,6 +1260,11 @@ constexpr int S_COL = S_LNROW + 256 * 8;       // bias [256] | LN colsum [256] (
 constexpr int S_STAT = S_COL + 2 * 256 * 4;    // residual epilogue: per (row, column wave) sum / M2 (8 KiB)
 constexpr int S_FLAG = S_STAT + 256 * 4 * 8;   // stream-K: the polled hand-off result, broadcast to the waves (16 B)
 constexpr int S_SMEM = S_FLAG + 16;             // 156 KiB + 16 B
+// MXFP8 operands (FP8 = 1, no stream-K): the E8M0 block scales of the ring's two K-tiles (A rows | W rows, 2 KiB
+// per slot) take the stream-K flag's place; 160 KiB in all.  The centred LayerNorm's per-row table (bf16 hi / lo of
+// mu_t - mean, 32 B per row) uses S_STAT, which only the residual epilogue needs otherwise.
+constexpr int S_MXS = S_FLAG;
+constexpr int S_SMEM_MX = S_MXS + 2 * 2048;
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt_n() {   // s_waitcnt vmcnt(N), N < 64
@@ -1326,6 +1340,19 @@ __device__ __forceinline__ void lds_rd_stat2(const void* p, f32x2 (&v)[4]) {
 __device__ __forceinline__ void lds_wr64(void* p, float2 v) {
   const f32x2 w = f32x2{v.x, v.y};
   asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(p)), "v"(w) : "memory");
+}
+__device__ __forceinline__ void lds_wr128(void* p, i32x4 v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+// 8 x 16 B at base + {0, 512, 1024, 1536, 4096, 4608, 5120, 5632} (a lane's 8 rows of the centred-LN row table)
+__device__ __forceinline__ void lds_rd_rowc(const void* p, i32x4 (&v)[8]) {
+  asm volatile(
+      "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:512\n\tds_read_b128 %2, %8 offset:1024\n\t"
+      "ds_read_b128 %3, %8 offset:1536\n\tds_read_b128 %4, %8 offset:4096\n\tds_read_b128 %5, %8 offset:4608\n\t"
+      "ds_read_b128 %6, %8 offset:5120\n\tds_read_b128 %7, %8 offset:5632\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(lds_addr(p))
+      : "memory");
 }
 // stream-K diagnostics (pdm_set_gemm_tuning bit 8): tails run, hand-offs not taken, summed poll time
 __device__ unsigned long long g_sk_stats[4];
@@ -1407,9 +1434,17 @@ __device__ __forceinline__ TV tile_view(const GemmArgs& p, const TV& t2, bool se
 //    waits unboundedly on another, and both branches give the same bits.
 // The producer's head runs first and needs nothing, so the flag is normally up long before the consumer's tail
 // (margin = share - nk K-steps); gemm_launch takes SK only where every workgroup's share is >= nk + 4 K-steps.
-template <int EPI, int MXO, int GRP, int SK = 0>
+//
+// FP8 = 1: MXFP8 operands (GemmArgs::fp8; gemm_mx_kernel's math on this ring): a K-tile is 128 e4m3 = the same
+// 128-byte rows, staged, swizzled and read exactly as the bf16 K-tile, one v_mfma_scale_f32_16x16x128_f8f6f4 per
+// fragment pair instead of two bf16 MFMAs, plus one 4-byte-per-lane LDS-DMA of E8M0 scales per wave and K-tile
+// (waves 0-3: the tile's A rows, 4-7: its W rows) issued with A0 W0 W1, so the ring waits count 9 ops instead of 8.
+// bf16 epilogue only, with the centred LayerNorm consumer (ln_gcol: acc += sum_t (mu_t - mean) c_t as one bf16 MFMA
+// per accumulator, as gemm_mx_kernel) or the plain one: the U-ViT-H/4 qkv.
+template <int EPI, int MXO, int GRP, int SK = 0, int FP8 = 0>
 __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int ntiles, const TV& p2, int nt0) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_RES, "persistent kernel epilogues");
+  static_assert(!FP8 || (EPI == EPI_BF16 && !MXO && !GRP && !SK), "MXFP8 operands: one-problem bf16 epilogue");
   static_assert(!MXO || EPI != EPI_RES, "MXFP8 output: bf16 / GELU epilogues");
   static_assert(!SK || !GRP, "stream-K: one problem");
   constexpr int ROWB = 128;
@@ -1419,6 +1454,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
   // VMEM ops every lane issues in an epilogue after its last wait: 16 output stores (+ 1 LN-partial store; MXO:
   // 16 fp8 row stores + 4 scale-byte stores)
   constexpr int E = EPI == EPI_RES ? 17 : MXO ? 20 : 16;
+  constexpr int ES = FP8 ? 1 : 2;   // operand bytes per element
+  constexpr int RW = FP8 ? 9 : 8;   // ring VMEM ops a lane leaves in flight at a phase wait (FP8: + the scale piece)
+  typedef int v8i __attribute__((ext_vector_type(8)));
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1432,7 +1470,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
   const int tstart = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
   const int tcnt = q8 + (x < r8 ? 1 : 0);
   const int nx = (G >> 3) + (x < (G & 7) ? 1 : 0);
-  const int nk = p.K / 64;   // >= 4 (gemm_launch)
+  const int nk = p.K / (FP8 ? 128 : 64);   // >= 4 (gemm_launch: fits_8s / fits_8s_mx)
   // segments: SK = 0 the tiles tstart + jw + i * nx (whole); SK = 1 [head of tile ht] [whole tiles tf0 ..] [tail]
   int ntl;
   int ht = 0, hke = 0, tf0 = 0, nf = 0, tt = 0, tkb = 0;
@@ -1502,10 +1540,19 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
   // come back as zeros, so the per-lane offsets below are the same for every tile
   const int ldw = p.ldw > 0 ? p.ldw : p.K;
   __amdgpu_buffer_rsrc_t ra1, ra2, rw;
+  // FP8: this wave's scale piece -- A rows (waves 0-3) or W rows (4-7) (wave & 3) * 64 + lane of the tile, zero past
+  // M / N (an E8M0 byte of 0xff would be NaN)
+  const bool s_is_a = wave < 4;
+  const int srow = (wave & 3) * 64 + lane;
+  unsigned soff = OOB;
   auto set_tile = [&](const TV& v, int m0_, int n0_) {
-    ra1 = make_rsrc(v.A1 + (size_t)m0_ * p.lda1, (long long)(v.M - m0_) * p.lda1 * 2);
-    ra2 = make_rsrc(v.A2 + (size_t)m0_ * p.lda1, (long long)(v.M - m0_) * p.lda1 * 2);
-    rw = make_rsrc(v.W + (size_t)n0_ * ldw, (long long)(p.N - n0_ - 1) * ldw * 2 + (long long)p.K * 2);
+    ra1 = make_rsrc(reinterpret_cast<const char*>(v.A1) + (size_t)m0_ * p.lda1 * ES, (long long)(v.M - m0_) * p.lda1 * ES);
+    ra2 = make_rsrc(reinterpret_cast<const char*>(v.A2) + (size_t)m0_ * p.lda1 * ES, (long long)(v.M - m0_) * p.lda1 * ES);
+    rw = make_rsrc(reinterpret_cast<const char*>(v.W) + (size_t)n0_ * ldw * ES,
+                   (long long)(p.N - n0_ - 1) * ldw * ES + (long long)p.K * ES);
+    if constexpr (FP8)
+      soff = s_is_a ? (m0_ + srow < v.M ? (unsigned)(m0_ + srow) * 4u : OOB)
+                    : (n0_ + srow < p.N ? (unsigned)(n0_ + srow) * 4u : OOB);
   };
   // output / residual / partials descriptors of the current tile's problem (rebuilt per tile: scalar work)
   __amdgpu_buffer_rsrc_t rout, rres, rst;
@@ -1529,8 +1576,8 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
     const unsigned sb = (unsigned)((pch ^ ((row >> 1) & 7)) * 16);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      aoff[h][i] = (unsigned)(h * 128 + row) * (unsigned)(p.lda1 * 2) + sb;
-      woff[h][i] = (unsigned)(h * 128 + row) * (unsigned)(ldw * 2) + sb;
+      aoff[h][i] = (unsigned)(h * 128 + row) * (unsigned)(p.lda1 * ES) + sb;
+      woff[h][i] = (unsigned)(h * 128 + row) * (unsigned)(ldw * ES) + sb;
     }
   }
   auto issue = [&](int slot, int kt, int kind) {
@@ -1542,6 +1589,18 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       if (kind >= KW0) dma16(rw, woff[kind - KW0][i], k0 * 2, d);
       else if (k0 < p.K1) dma16(ra1, aoff[kind][i], k0 * 2, d);
       else dma16(ra2, aoff[kind][i], (k0 - p.K1) * 2, d);
+    }
+  };
+  // FP8: the E8M0 scales of K-tile kt into ring slot `slot` (one 4-byte piece per lane: 256 rows per wave group)
+  const __amdgpu_buffer_rsrc_t rsa =
+      make_rsrc(FP8 ? (const void*)p.a_scale : (const void*)p.W, FP8 ? (long long)nk * p.a_scale_ld * 4 : 0);
+  const __amdgpu_buffer_rsrc_t rsw =
+      make_rsrc(FP8 ? (const void*)p.w_scale : (const void*)p.W, FP8 ? (long long)nk * p.w_scale_ld * 4 : 0);
+  auto issue_scales = [&](int slot, int kt) {
+    if constexpr (FP8) {
+      PDM_LDS void* d = (PDM_LDS void*)(smem + S_MXS + slot * 2048 + (s_is_a ? 0 : 1024) + (wave & 3) * 256);
+      if (s_is_a) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, d, 4, (int)soff, kt * p.a_scale_ld * 4, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, d, 4, (int)soff, kt * p.w_scale_ld * 4, 0, 0);
     }
   };
   // a tile's small tables -> LDS by buffer LDS-DMA (zeros past M / N; hipcc orders LDS reads behind these without
@@ -1581,6 +1640,24 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
         wf[qj][ni][ks] = *reinterpret_cast<const bf16x8*>(buf + (2 + qj) * HALF + swz_off<64>(row, ks * 4 + g4));
       }
   };
+  // FP8: the same chunks read straight into 8-VGPR operands (the scaled MFMA takes 32 bytes per lane; two bf16x8
+  // halves would need copies into adjacent registers)
+  v8i af8[4], wf8[2][2];
+  auto frag8 = [&](v8i& dst, const char* base, int row) {
+    i32x4* h = reinterpret_cast<i32x4*>(&dst);
+    h[0] = *reinterpret_cast<const i32x4*>(base + swz_off<64>(row, g4));
+    h[1] = *reinterpret_cast<const i32x4*>(base + swz_off<64>(row, 4 + g4));
+  };
+  auto read_a8 = [&](const char* buf, int qi) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) frag8(af8[mi], buf + qi * HALF, wm * 64 + mi * 16 + r16);
+  };
+  auto read_w8 = [&](const char* buf) {
+#pragma unroll
+    for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) frag8(wf8[qj][ni], buf + (2 + qj) * HALF, wn * 32 + ni * 16 + r16);
+  };
   auto lds_done = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -1599,6 +1676,45 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
         }
     __builtin_amdgcn_s_setprio(0);
   };
+  // FP8: a lane's packed E8M0 bytes (gemm_mx_kernel's read_scales): sa[qi] byte mi, sw byte qj * 2 + ni, each the
+  // lane's k-block g4 of its row
+  unsigned sa[2] = {0u, 0u}, sw = 0u;
+  auto read_scales = [&](int slot) {
+    const unsigned* sl = reinterpret_cast<const unsigned*>(smem + S_MXS + slot * 2048);
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+      unsigned v = 0;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) v |= ((sl[qi * 128 + wm * 64 + mi * 16 + r16] >> (8 * g4)) & 0xffu) << (8 * mi);
+      sa[qi] = v;
+    }
+    unsigned v = 0;
+#pragma unroll
+    for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        v |= ((sl[256 + qj * 128 + wn * 32 + ni * 16 + r16] >> (8 * g4)) & 0xffu) << (8 * (qj * 2 + ni));
+    sw = v;
+    asm volatile("" : "+v"(sa[0]), "+v"(sa[1]), "+v"(sw));
+  };
+  // FP8: one scaled MFMA per fragment pair (the lane's 32-byte fragments = chunks g4 and 4 + g4 of its row)
+  auto mma8 = [&](auto qic, auto qjc) {
+    constexpr int qi = decltype(qic)::value, qj = decltype(qjc)::value;
+    __builtin_amdgcn_s_setprio(1);
+    static_for<2>([&](auto nic) {
+      constexpr int ni = decltype(nic)::value;
+      static_for<4>([&](auto mic) {
+        constexpr int mi = decltype(mic)::value;
+        f32x4& c = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
+        c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf8[qj][ni], af8[mi], c, 0, 0, qj * 2 + ni, sw, mi,
+                                                             sa[qi]);
+        asm volatile("" : "+v"(c));   // keep the MFMA in this phase (as gemm_mx_kernel)
+      });
+    });
+    __builtin_amdgcn_s_setprio(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
 
   int m0, n0;
   bool sec;
@@ -1611,14 +1727,16 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
   // prologue of the first segment: tables, K-tile kb, A0 W0 W1 of K-tile kb+1; the wait retires the tables and
   // A0 W0 W1(kb)
   issue_tables(cv, m0, n0);
+  issue_scales(0, kb);
   issue(0, kb, KA0);
   issue(0, kb, KW0);
   issue(0, kb, KW1);
   issue(0, kb, KA1);
+  issue_scales(1, kb + 1);
   issue(1, kb + 1, KA0);
   issue(1, kb + 1, KW0);
   issue(1, kb + 1, KW1);
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  wait_vmcnt_n<RW>();
   bar_raw();
 
   int g = 0;                  // K-steps run so far: the ring slot of the next one is g & 1
@@ -1710,34 +1828,47 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       const bool m1 = kt + 1 < ke || has_next;   // K-tile g+1 exists (this segment's kt+1 or the next one's kbn)
       const bool m2 = kt + 2 < ke || has_next;   // K-tile g+2 (segments >= 2 K-tiles: the next one's kbn + {0, 1})
       // phase A: quadrants (0,0) (0,1); issues A1 of K-tile g+1
-      read_a(buf, 0);
-      read_w(buf, 0);
-      read_w(buf, 1);
+      if constexpr (FP8) {
+        read_a8(buf, 0);
+        read_w8(buf);
+        read_scales(slot);
+      } else {
+        read_a(buf, 0);
+        read_w(buf, 0);
+        read_w(buf, 1);
+      }
       lds_done();
       if (m1) {
         issue(slot ^ 1, kt + 1 < ke ? kt + 1 : kbn, KA1);
         if (first && after_slab) wait_vmcnt_n<8 + 32>();
-        else if (first) wait_vmcnt_n<8 + E>();
-        else wait_vmcnt_n<8>();
+        else if (first) wait_vmcnt_n<RW + E>();
+        else wait_vmcnt_n<RW>();
       } else {
         wait_vmcnt_n<0>();
       }
       bar_raw();
-      mma(0, 0);
-      mma(0, 1);
+      if constexpr (FP8) {
+        mma8(I0{}, I0{});
+        mma8(I0{}, I1{});
+      } else {
+        mma(0, 0);
+        mma(0, 1);
+      }
       bar_raw();
       // phase B: quadrants (1,0) (1,1); issues A0 W0 W1 of K-tile g+2 (the next segment's from kt = ke-2 on)
-      read_a(buf, 1);
+      if constexpr (FP8) read_a8(buf, 1);
+      else read_a(buf, 1);
       lds_done();
       if (kt == ke - 2 && has_next) set_tile(nv, m0n, n0n);
       if (m2) {
         const int k2 = kt + 2 < ke ? kt + 2 : kbn + (kt + 2 - ke);
+        issue_scales(slot, k2);
         issue(slot, k2, KA0);
         issue(slot, k2, KW0);
         issue(slot, k2, KW1);
         if (first && after_slab) wait_vmcnt_n<8 + 32>();
-        else if (first) wait_vmcnt_n<8 + E>();
-        else wait_vmcnt_n<8>();
+        else if (first) wait_vmcnt_n<RW + E>();
+        else wait_vmcnt_n<RW>();
       } else if (m1) {
         wait_vmcnt_n<2>();
       }
@@ -1747,8 +1878,13 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       if constexpr (SK) {
         if (pub_pending && kt == kb + 1) publish();
       }
-      mma(1, 0);
-      mma(1, 1);
+      if constexpr (FP8) {
+        mma8(I1{}, I0{});
+        mma8(I1{}, I1{});
+      } else {
+        mma(1, 0);
+        mma(1, 1);
+      }
       bar_raw();
     }
     if (wave < 4) bar_raw();   // rejoin the stagger
@@ -1797,13 +1933,31 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
     const int tid_e = opaque_i(tid), g4e = (tid_e & 63) >> 4, r16e = tid_e & 15;
     lds_rd_cols(smem + S_COL + (wn * 32 + g4e * 4) * 4, bv, cs);
     char* lnrow = smem + S_LNROW;
+    // FP8 centred LayerNorm (ln_gcol): rows carry mean 0 and the table of (mu_t - mean) as bf16 hi / lo
+    const bool lnc = FP8 && ln && p.ln_gcol != nullptr;
     if (ln && tid < 256) {
       f32x2 raw[8];
       lds_rd_raw(smem + S_RAW + tid_e * p.ln_ld * 8, raw);
       float2 lst[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) lst[t] = t < p.ln_ld ? make_float2(raw[t][0], raw[t][1]) : make_float2(0.f, 0.f);
-      lds_wr64(lnrow + tid * 8, ln_from_partials(lst, p.ln_ld, p.ln_D, p.ln_eps, nullptr));
+      if (lnc) {
+        float mu[8];
+        const float2 mr = ln_from_partials(lst, p.ln_ld, p.ln_D, p.ln_eps, mu);
+        unsigned hl[8];   // hi pairs 0..3, lo pairs 4..7
+#pragma unroll
+        for (int t = 0; t < 8; t += 2) {
+          const float d0 = mu[t] - mr.x, d1 = mu[t + 1] - mr.x;
+          const unsigned h = pack_bf16x2(d0, d1);
+          hl[t >> 1] = h;
+          hl[4 + (t >> 1)] = pack_bf16x2(d0 - bf16lo(h), d1 - bf16hi(h));
+        }
+        lds_wr128(smem + S_STAT + tid * 32, i32x4{(int)hl[0], (int)hl[1], (int)hl[2], (int)hl[3]});
+        lds_wr128(smem + S_STAT + tid * 32 + 16, i32x4{(int)hl[4], (int)hl[5], (int)hl[6], (int)hl[7]});
+        lds_wr64(lnrow + tid * 8, make_float2(0.f, mr.y));
+      } else {
+        lds_wr64(lnrow + tid * 8, ln_from_partials(lst, p.ln_ld, p.ln_D, p.ln_eps, nullptr));
+      }
     }
     lds_sync();
 #pragma unroll
@@ -1811,9 +1965,43 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
         if (!p.bias) bv[qj][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (!ln) cs[qj][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!ln || lnc) cs[qj][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     bar_raw();   // lnrow complete; the raw / column tables are free for the next tile's
+    if constexpr (FP8) {
+      if (lnc) {
+        // acc += sum_t (mu_t - mean) c_t[n] as one bf16 16x16x32 MFMA per accumulator (gemm_mx_kernel's correction):
+        // K lanes 0-7 carry hi * hi, 8-15 hi * lo, 16-23 lo * hi, 24-31 zeros.  Column tables c_t (hi | lo, 32 B per
+        // column) come straight from ln_gcol, the row tables from S_STAT.
+        const __amdgpu_buffer_rsrc_t rg = make_rsrc(p.ln_gcol, (long long)p.N * 32);
+        i32x4 gv[2][2];
+#pragma unroll
+        for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni) {
+            const int col = n0 + qj * 128 + wn * 32 + ni * 16 + r16e;
+            const unsigned off = (g4e == 3 || col >= p.N) ? OOB : (unsigned)col * 32u + (g4e == 1 ? 16u : 0u);
+            gv[qj][ni] = __builtin_amdgcn_raw_buffer_load_b128(rg, (int)off, 0, 0);
+          }
+        i32x4 rv[8];
+        lds_rd_rowc(smem + S_STAT + (wm * 64 + r16e) * 32 + (g4e == 2 ? 16 : 0), rv);
+        wait_vmcnt_n<0>();
+        asm volatile("" : "+v"(gv[0][0]), "+v"(gv[0][1]), "+v"(gv[1][0]), "+v"(gv[1][1]));
+        const i32x4 z4 = i32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+          for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+              for (int mi = 0; mi < 4; ++mi) {
+                f32x4& c = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
+                const i32x4 a = g4e == 3 ? z4 : rv[qi * 4 + mi];
+                c = mfma16x16x32(__builtin_bit_cast(bf16x8, gv[qj][ni]), __builtin_bit_cast(bf16x8, a), c);
+              }
+      }
+    }
     if (has_next) issue_tables(nv, m0n, n0n);
     const int offg = (g4 & 1) * 16 + (g4 >> 1) * 8;   // post-swap column offset of the lane's 8 columns
     float2 mrow[2][4];   // (mean, rstd) of the lane's 8 rows
@@ -2024,9 +2212,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
 
 // the one-problem kernel keeps its own signature (a second by-value GemmArgs in every launch measured +0.7 % on the
 // L/2 forward); the grouped kernel takes both problems
-template <int EPI, int MXO = 0, int SK = 0>
+template <int EPI, int MXO = 0, int SK = 0, int FP8 = 0>
 __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n, int ntiles) {
-  gemm8s_body<EPI, MXO, 0, SK>(p, tiles_n, ntiles, TV{}, ntiles);
+  gemm8s_body<EPI, MXO, 0, SK, FP8>(p, tiles_n, ntiles, TV{}, ntiles);
 }
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm8g_kernel(GemmArgs p, int tiles_n, int ntiles, TV p2, int nt0) {
@@ -2246,14 +2434,6 @@ __global__ __launch_bounds__(512, 1) void gemm8t_kernel(GemmArgs p, int nwg) {
 // E8M0 bytes it needs per operand half into one VGPR and the MFMA selects them with opsel.
 //   phase A(k): reads A0 W0 W1 + scales of tile k, issues A1(k+1)          wait: A1(k)
 //   phase B(k): reads A1,      issues S A0 W0 W1 of tile k+2               wait: S A0 W0 W1 (k+1)
-template <int... I, class F>
-__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, I...>, F&& f) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  sfor_impl(std::make_integer_sequence<int, N>{}, f);
-}
 
 constexpr int MX_SCALE_LDS = EPI_LDS + EPI_LDS_EXTRA;   // 2 x 2 KiB of staged block scales
 constexpr int MX_COL_LDS = MX_SCALE_LDS + 2 * 2048;      // the tile's bias [256] + LN colsum [256] (fp32)
@@ -2826,7 +3006,7 @@ static bool persist_kernels_ok() {
                          (const void*)gemm8s_kernel<EPI_GELU, 0, 1>, (const void*)gemm8s_kernel<EPI_RES, 0, 1>,
                          (const void*)gemm8s_kernel<EPI_BF16, 1, 1>, (const void*)gemm8s_kernel<EPI_GELU, 1, 1>,
                          (const void*)gemm8g_kernel<EPI_BF16>, (const void*)gemm8g_kernel<EPI_GELU>,
-                         (const void*)gemm8g_kernel<EPI_RES>};
+                         (const void*)gemm8g_kernel<EPI_RES>, (const void*)gemm8s_kernel<EPI_BF16, 0, 0, 1>};
     ok = 1;
     for (const void* f : fns) {
       hipFuncAttributes at{};
@@ -2860,6 +3040,37 @@ static bool fits_8s(const GemmArgs& p, int epi) {
   if (p.stats_out && (long long)p.M * p.stats_ld * 8 >= lim) return false;
   if (p.dbg_tile0 & 15) return false;   // gemm8d's timing modes
   return fits_rsrc(p);
+}
+
+// the persistent kernel's MXFP8-operand form (gemm8s_kernel<EPI_BF16, 0, 0, 1>, algo 11 only): the bf16 epilogue with
+// or without the (centred) LayerNorm consumer -- the U-ViT-H/4 qkv; everything else keeps gemm_mx_kernel
+static bool fits_8s_mx(const GemmArgs& p, int epi) {
+  const long long lim = 0x7fffffffLL;
+  if (!persist_kernels_ok()) return false;
+  if (epi != EPI_BF16 || !p.fp8 || p.out_fp8 || p.A2 || p.K1 != p.K || p.conv || p.batch > 1 || p.a_rows_per_group > 0)
+    return false;
+  if (!p.out_bf16 || p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15) || p.K % 128 || p.K < 512) return false;
+  if (p.ln_stats && p.ln_ld > 8) return false;
+  if ((long long)p.M * p.ldo * 2 >= lim || (p.dbg_tile0 & 15)) return false;
+  return fits_rsrc(p);
+}
+
+static hipError_t launch8s_mx(const GemmArgs& p, hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 0, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              S_SMEM_MX);
+    attr_set = true;
+  }
+  if (g_num_cus == 0) {   // as launch8s
+    int dev = 0, n = 0;
+    g_num_cus = (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) ? n : 256;
+  }
+  const int tn = (p.N + BN2 - 1) / BN2, tm = (p.M + BM2 - 1) / BM2;
+  const int ntiles = tm * tn;
+  const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
+  hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 0, 0, 1>), dim3(grid), dim3(512), S_SMEM_MX, stream, p, tn, ntiles);
+  return hipGetLastError();
 }
 
 static hipError_t launch_mx(const GemmArgs& p, int epi, hipStream_t stream) {
@@ -2956,6 +3167,9 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
                          (p.out_bf16 && (p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))))) algo = 1;
   if (p.fp8) {
     if (!fits_rsrc(p)) return hipErrorInvalidValue;
+    // the persistent form on request only (algo 11): measured 3.5-4.7 % slower than gemm_mx_kernel on the H/4 qkv
+    // at 50-190 rows (tools/mx_qkv_bench.py), so the automatic choice stays one tile per workgroup
+    if (g_gemm_algo == 11 && fits_8s_mx(p, epi)) return launch8s_mx(p, stream);
     return launch_mx(p, epi, stream);
   }
   if (p.out_fp8) algo = 7;   // MXFP8 output lives in the 256-tile epilogue

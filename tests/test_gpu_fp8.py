@@ -128,6 +128,45 @@ def test_mx_only_output_bit_exact(lib, algo, epi, ln, M, N, K):
     assert bool((s[:, M:] == -1).all())
 
 
+@pytest.mark.parametrize("M,N,K", [(4133, 1152, 1152), (12900, 3456, 1152), (5000, 256, 512), (4096, 520, 1152)])
+@pytest.mark.parametrize("centred", [False, True])
+def test_mx_persistent_vs_tile_kernel(lib, M, N, K, centred):
+    """The persistent kernel's MXFP8-operand form (gemm8s_kernel FP8 = 1, algo 11; measured slower than the tile
+    kernel, so not automatic) against gemm_mx_kernel (algo 7 = auto, one tile per workgroup) on the same operands:
+    the same K-ordered chain of scaled MFMAs per accumulator, so the plain bf16 + bias epilogue is bit-identical; with
+    the centred LayerNorm consumer (ln_stats + ln_gcol, the correction MFMA) both compute rstd * acc + bias,
+    compared at 1e-3.  Ragged M / N tiles (N = 1152: 4.5 column tiles; N = 520: a 256 + 256 + 8 split) included."""
+    from panopticdiffusionmodels_amd.native import gcol_table
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + int(centred))
+    x = torch.randn(M, K, device="cuda", generator=g) * 1.5 + 3.0
+    w = torch.randn(N, K, device="cuda", generator=g) * K ** -0.5
+    bias = torch.randn(N, device="cuda", generator=g)
+    qw, sw, dw = _mx(lib, w)
+    kw = {}
+    if centred:
+        _, st = lib.rowstats(x, want_bf16=False)
+        qx, sx = lib.mx_quantize_centred(x, st)
+        kw = dict(ln_stats=st, ln_colsum=dw.double().sum(1).float(), ln_gcol=gcol_table(dw))
+    else:
+        qx, sx, _ = _mx(lib, x)
+    outs = {}
+    try:
+        for algo in (7, 11):
+            lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
+            out = torch.full((M, N + 8), 7.0, device="cuda", dtype=torch.bfloat16)   # ldo = N + 8: pad untouched
+            lib.gemm_ex(lib.EPI_BF16, qx, qw, bias, sx, sw, out=out[:, :N], **kw)
+            outs[algo] = out
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+    assert bool((outs[11][:, N:] == 7.0).all())
+    a, b = outs[11][:, :N].float(), outs[7][:, :N].float()
+    assert torch.isfinite(a).all()
+    if centred:
+        assert rel(a, b) < 1e-3
+    else:
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("centred,offset", [(False, 0.0), (True, 0.0), (True, 2.0), (True, 8.0), (True, 32.0)])
 def test_mxfp8_layernorm_consumer_chain(lib, centred, offset):
     """fc1 of a U-ViT-H block in fp8: MX(x) operand + gamma-folded MX weight + fused LayerNorm + GELU, emitting
