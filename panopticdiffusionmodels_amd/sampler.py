@@ -60,8 +60,22 @@ def _drop_stale_graph(st, nnet):
 def _lane_streams(owner, main):
     """Streams of the concurrent lanes: lane 0 runs on the caller's stream, lanes 1.. on the process's shared side
     streams (_lib.lane_streams: high priority, so a lane never waits behind another lane's kernels in a shared
-    hardware queue)."""
+    hardware queue).  Lane 0 on a side stream as well (equal priorities) measured 0.2-0.3 % slower."""
     return [main] + _lib.lane_streams(main.device, owner.lanes - 1)
+
+
+def _fork(main, streams):
+    for s in streams:
+        if s is not main:
+            s.wait_stream(main)
+
+
+def _join(main, streams, outs):
+    for s, o in zip(streams, outs):
+        if s is not main:
+            main.wait_stream(s)
+            for t in (o if isinstance(o, tuple) else (o,)):
+                t.record_stream(main)
 
 
 class ClassCondSampler:
@@ -145,8 +159,7 @@ class ClassCondSampler:
     def _sample_lanes(self, z, y):
         main = torch.cuda.current_stream(z.device)
         streams = _lane_streams(self, main)
-        for s in streams[1:]:
-            s.wait_stream(main)   # before lane 0's work is queued on main
+        _fork(main, streams)   # before lane 0's work is queued on main
         bounds = [round(i * z.shape[0] / self.lanes) for i in range(self.lanes + 1)]
         outs = []
         for i, s in enumerate(streams):
@@ -154,9 +167,7 @@ class ClassCondSampler:
                 zi = z[bounds[i]:bounds[i + 1]]
                 yi = y[bounds[i]:bounds[i + 1]] if y is not None else None
                 outs.append(self._sample_one(zi, yi, False, lane=i))
-        for s, o in zip(streams[1:], outs[1:]):
-            main.wait_stream(s)
-            o.record_stream(main)
+        _join(main, streams, outs)
         return torch.cat(outs)
 
     def _sample_one(self, z, y, eager, lane=None):
@@ -270,18 +281,14 @@ class T2ISampler:
         if self.lanes > 1 and B >= self.lanes and self.use_graph:
             main = torch.cuda.current_stream(z.device)
             streams = _lane_streams(self, main)
-            for s in streams[1:]:
-                s.wait_stream(main)
+            _fork(main, streams)
             bounds = [round(i * B / self.lanes) for i in range(self.lanes + 1)]
             outs = []
             for i, s in enumerate(streams):
                 lo, hi = bounds[i], bounds[i + 1]
                 with torch.cuda.stream(s):
                     outs.append(self._sample_one(z[lo:hi], context[lo:hi], empty_context, mask_token[lo:hi], i))
-            for s, (a, b) in zip(streams[1:], outs[1:]):
-                main.wait_stream(s)
-                a.record_stream(main)
-                b.record_stream(main)
+            _join(main, streams, outs)
             return torch.cat([a for a, _ in outs]), torch.cat([b for _, b in outs])
         return self._sample_one(z, context, empty_context, mask_token)
 
