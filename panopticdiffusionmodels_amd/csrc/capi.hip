@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -39,6 +40,12 @@ namespace {
   do {                                                                                  \
     hipError_t e_ = (call);                                                             \
     if (e_ != hipSuccess) return fail(PDM_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define PDM_TRY(x)           \
+  do {                       \
+    int r_ = (x);            \
+    if (r_) return r_;       \
   } while (0)
 
 #define PDM_CHECK(msg_expr)                          \
@@ -158,11 +165,6 @@ struct Workspace {
   Q8 xtq;            // block-internal x (skip_linear / proj epilogues: qkv / fc1 operand) [rows*Lx, D]
   Q8 atq;            // attention output (proj operand)                                  [rows*Lx, D]
   Q8 mlq;            // GELU(fc1) (fc2 operand)                                          [rows*Lx, Hid]
-  // stream-K state of the persistent GEMM (pdm::GemmArgs::sk_flags / sk_slab): SK_LAUNCHES blocks of 256 flag words
-  // (one block per GEMM launch of a forward, zeroed at the start of every forward) + one 64 MiB accumulator slab
-  // reused by every launch (stream order)
-  unsigned* SKF;
-  float* SKS;
   size_t bytes;
 };
 
@@ -224,9 +226,7 @@ Workspace layout(const pdm_uvit* h, int rows, char* base) {
       w.MLP2 = (bf16*)take(Mx * h->Hid * 2);
     }
   }
-  w.SKF = (unsigned*)take((size_t)SK_LAUNCHES * pdm::SK_FLAG_WORDS * 4);
-  w.SKS = (float*)take((size_t)pdm::SK_SLAB_BYTES);
-  w.bytes = off;
+  w.bytes = off;   // (stream-K's flags and slab are library-owned per stream: sk_state)
   return w;
 }
 
@@ -240,14 +240,59 @@ struct Ctx {
   int* skn = nullptr;
 };
 
-// a forward's stream-K state: its flag blocks zeroed on the stream first (one memset node in a captured graph); none
-// while the policy is off (a graph captured then keeps whole tiles)
-int sk_begin(Ctx& c, const Workspace& w, int* counter) {
+// Stream-K state of the persistent GEMM (pdm::GemmArgs::sk_flags / sk_slab): SK_RING blocks of SK_FLAG_WORDS flag
+// words (one block per GEMM launch) + one 64 MiB fp32 accumulator slab reused launch after launch in stream order.
+// Owned by the library, one state per (device, stream), allocated on first use -- stream-K is off by default, so no
+// forward workspace carries its 64 MiB, every device has its own (a process driving several GPUs), and
+// concurrent streams (the sampling lanes) never share a slab.  Never allocated inside a stream capture: a forward
+// captured on a stream without a state keeps whole tiles.
+constexpr int SK_RING = 4096;
+struct SkState {
+  unsigned* flags = nullptr;
+  float* slab = nullptr;
+  int next = 0;   // next free flag block (host order of the launches on this stream); blocks past it are zero
+};
+static std::mutex g_sk_mu;
+static std::map<std::pair<int, hipStream_t>, SkState> g_sk_state;
+
+static int sk_state(hipStream_t s, SkState** out) {
+  *out = nullptr;
+  int dev = 0;
+  PDM_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(g_sk_mu);
+  auto it = g_sk_state.find({dev, s});
+  if (it == g_sk_state.end()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    PDM_HIP(hipStreamIsCapturing(s, &cs));
+    if (cs != hipStreamCaptureStatusNone) return PDM_OK;   // no allocation inside a capture: whole tiles
+    SkState st;
+    PDM_HIP(hipMalloc(&st.flags, (size_t)SK_RING * pdm::SK_FLAG_WORDS * 4));
+    PDM_HIP(hipMalloc(&st.slab, (size_t)pdm::SK_SLAB_BYTES));
+    PDM_HIP(hipMemsetAsync(st.flags, 0, (size_t)SK_RING * pdm::SK_FLAG_WORDS * 4, s));
+    it = g_sk_state.emplace(std::make_pair(dev, s), st).first;
+  }
+  *out = &it->second;
+  return PDM_OK;
+}
+
+// a forward's stream-K state: SK_LAUNCHES flag blocks of the stream's ring, zeroed on the stream first (one memset
+// node in a captured graph, so every replay starts from zeroed flags); none while the policy is off (a graph
+// captured then keeps whole tiles)
+int sk_begin(Ctx& c, int* counter) {
   *counter = 0;
   if (pdm::gemm_get_sk() == 0) return PDM_OK;
-  PDM_HIP(hipMemsetAsync(w.SKF, 0, (size_t)SK_LAUNCHES * pdm::SK_FLAG_WORDS * 4, c.s));
-  c.skf = w.SKF;
-  c.sks = w.SKS;
+  SkState* st = nullptr;
+  PDM_TRY(sk_state(c.s, &st));
+  if (!st) return PDM_OK;
+  if (st->next + SK_LAUNCHES > SK_RING) {   // wrap: the whole ring zeroed, so blocks past `next` stay clean
+    PDM_HIP(hipMemsetAsync(st->flags, 0, (size_t)SK_RING * pdm::SK_FLAG_WORDS * 4, c.s));
+    st->next = 0;
+  }
+  unsigned* f = st->flags + (size_t)st->next * pdm::SK_FLAG_WORDS;
+  st->next += SK_LAUNCHES;
+  PDM_HIP(hipMemsetAsync(f, 0, (size_t)SK_LAUNCHES * pdm::SK_FLAG_WORDS * 4, c.s));
+  c.skf = f;
+  c.sks = st->slab;
   c.skn = counter;
   return PDM_OK;
 }
@@ -373,12 +418,6 @@ int gemm8(const Ctx& c, const Q8& A, const std::string& wkey, const float* bias,
   a.res_in = res_in; a.ldri = res_in ? N : 0;
   return launch_gemm(c, a, epi);
 }
-
-#define PDM_TRY(x)           \
-  do {                       \
-    int r_ = (x);            \
-    if (r_) return r_;       \
-  } while (0)
 
 // One U-ViT Block (libs/uvit.py:115-120) on `rows_L` token rows of width D held in X (fp32), with norm1 /
 // norm2 fused into qkv / fc1 (GemmArgs): on entry xb_in = bf16(X) and st_in = the LayerNorm partials of X;
@@ -1120,7 +1159,7 @@ int pdm_uvit_forward(pdm_uvit* h, const float* x, const float* t, const int64_t*
   h->prof_n = 0;
   Ctx c{h, (hipStream_t)stream};
   int skn = 0;
-  PDM_TRY(sk_begin(c, w, &skn));
+  PDM_TRY(sk_begin(c, &skn));
   const int D = h->D, L = h->Lx;
   {
     pdm::AssembleArgs a{};
@@ -1163,7 +1202,7 @@ int pdm_uvit_t2i_forward(pdm_uvit* h, const float* x, const float* t, const floa
   h->prof_n = 0;
   Ctx c{h, (hipStream_t)stream};
   int skn = 0;
-  PDM_TRY(sk_begin(c, w, &skn));
+  PDM_TRY(sk_begin(c, &skn));
   const int D = h->D, Lx = h->Lx, Lm = h->Lm, nctx = h->cfg.num_clip_token;
   // context_embed (libs/uvit_t2i.py:387): bf16 cast + GEMM (+bias) -> fp32 context tokens
   PDM_HIP(pdm::cast_bf16_launch(context, w.CTXB, (long long)rows * nctx * h->cfg.clip_dim, c.s));
@@ -1321,24 +1360,18 @@ int pdm_rowstats(const float* x, int ldx, int rows, int D, void* xb, float* stat
   return PDM_OK;
 }
 
-// stream-K state for standalone pdm_gemm calls (pdm_set_gemm_sk mode bit 2; tests and tools, ONE stream at a time):
-// a ring of flag blocks, zeroed whenever it wraps, and one slab
+// stream-K state for standalone pdm_gemm calls (pdm_set_gemm_sk mode bit 2; tests and tools): the calling stream's
+// ring (sk_state), its next flag block per call, the ring zeroed on the stream whenever it wraps
 static int sk_standalone(pdm::GemmArgs& a, hipStream_t s) {
-  constexpr int RING = 4096;
-  static unsigned* flags = nullptr;
-  static float* slab = nullptr;
-  static int next = 0;
-  if (!flags) {
-    PDM_HIP(hipMalloc(&flags, (size_t)RING * pdm::SK_FLAG_WORDS * 4));
-    PDM_HIP(hipMalloc(&slab, (size_t)pdm::SK_SLAB_BYTES));
-    PDM_HIP(hipMemset(flags, 0, (size_t)RING * pdm::SK_FLAG_WORDS * 4));
+  SkState* st = nullptr;
+  PDM_TRY(sk_state(s, &st));
+  if (!st) return PDM_OK;   // capturing without a state: whole tiles
+  if (st->next == SK_RING) {
+    PDM_HIP(hipMemsetAsync(st->flags, 0, (size_t)SK_RING * pdm::SK_FLAG_WORDS * 4, s));
+    st->next = 0;
   }
-  if (next == RING) {
-    PDM_HIP(hipMemsetAsync(flags, 0, (size_t)RING * pdm::SK_FLAG_WORDS * 4, s));
-    next = 0;
-  }
-  a.sk_flags = flags + (size_t)next++ * pdm::SK_FLAG_WORDS;
-  a.sk_slab = slab;
+  a.sk_flags = st->flags + (size_t)st->next++ * pdm::SK_FLAG_WORDS;
+  a.sk_slab = st->slab;
   return PDM_OK;
 }
 

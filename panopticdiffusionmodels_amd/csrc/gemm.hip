@@ -1741,6 +1741,13 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
 
   int g = 0;                  // K-steps run so far: the ring slot of the next one is g & 1
   bool pub_pending = false;   // SK: this workgroup's head slab stored, its flag not yet raised
+  // Ordering of the hand-off (relaxed atomics by design): publish() runs only after EVERY wave of this
+  // workgroup has drained its slab stores (wait_vmcnt_n<0> + barrier in the tail branch below; the stores are sc1
+  // write-through, so vmcnt 0 means they reached this XCD's L2), and the consumer is workgroup blockIdx + 8, which
+  // the round-robin dispatch places on the SAME XCD (blockIdx % 8) and hence the same L2; it polls with agent-scope
+  // loads and reads the slab with sc1 (L1-bypassing) loads after a barrier.  An __ATOMIC_RELEASE store at agent scope
+  // would add an L2 writeback (buffer_wbl2) of every dirty line for other XCDs that never read the slab.  If the
+  // workgroup -> XCD mapping ever changes, switch to release / acquire.  Off by default (pdm_set_gemm_sk).
   auto publish = [&]() {
     if (tid == 0) __hip_atomic_store(p.sk_flags + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     pub_pending = false;

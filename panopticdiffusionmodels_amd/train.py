@@ -222,23 +222,47 @@ class HipTrainState:
         t_in = t_in.to(self.device, torch.float32).contiguous().reshape(B)
         if y is not None:
             # the reference's nn.Embedding raises IndexError on an out-of-range label; the kernels would read the
-            # neighbouring parameter (pos_embed) as the embedding and scatter its gradient there, so check here --
-            # host-side labels only (the data loader's): a check of device-resident labels would synchronise the
-            # stream every step
+            # neighbouring parameter (pos_embed) as the embedding and scatter its gradient there.  Host labels (the
+            # data loader's) are checked here; device-resident labels are clamped into range on the stream (the
+            # kernels never read outside label_emb) and their range error is kept in a device flag that
+            # _raise_label_error reads once the step that set it has finished -- no synchronisation per step
             nc = int(self.kw.get("num_classes", -1))
             if nc <= 0:
                 raise ValueError("HipTrainState: labels given to an unconditional U-ViT (num_classes <= 0)")
+            self._raise_label_error(block=False)
             if y.numel() and y.device.type == "cpu":
                 lo, hi = (int(v) for v in torch.stack([y.min(), y.max()]).cpu())
                 if lo < 0 or hi >= nc:
                     raise IndexError(f"HipTrainState: label out of range [0, {nc}): min {lo}, max {hi}")
-            y = y.to(self.device, torch.int64).contiguous()
+                y = y.to(self.device, torch.int64).contiguous()
+            elif y.numel():
+                y = y.to(self.device, torch.int64)
+                bad = ((y < 0) | (y >= nc)).any()
+                self._label_bad = bad if getattr(self, "_label_bad", None) is None else self._label_bad | bad
+                self._label_ev = torch.cuda.Event()
+                self._label_ev.record(torch.cuda.current_stream(self.device))
+                y = y.clamp(0, nc - 1).contiguous()
+            else:
+                y = y.to(self.device, torch.int64).contiguous()
         gs = float(1.0 / B if gscale is None else gscale)
         loss = torch.empty(B, dtype=torch.float32, device=self.device)
         self._lanes(B, lambda h, a, b, ws, s: self._step_call(h, xt[a:b], t_in[a:b], y[a:b] if y is not None else None,
                                                               target[a:b], loss[a:b], gs, ws, s),
                     (xt, t_in, target, loss) + ((y,) if y is not None else ()))
         return loss
+
+    def _raise_label_error(self, block=True):
+        """IndexError if a device-resident label of an earlier step was out of range [0, num_classes) (those steps ran
+        on clamped labels).  block=False reads the flag only once the step that set it has finished."""
+        bad = getattr(self, "_label_bad", None)
+        if bad is None or (not block and not self._label_ev.query()):
+            return
+        self._label_bad = None
+        if bool(bad):
+            raise IndexError(f"HipTrainState: a device label of an earlier step was out of range "
+                             f"[0, {int(self.kw.get('num_classes', -1))}) (that step ran on clamped labels)")
+
+    check_labels = _raise_label_error
 
     def _lanes(self, B, call, tensors):
         """call(handle, row0, row1, workspace, stream) for the whole batch on the current stream, or (lanes = 2) for

@@ -156,3 +156,22 @@ def test_fp8_param_table_without_gpu():
         k2["fp8"] = True
         with pytest.raises(ValueError):
             _lib.check(lib.pdm_uvit_create(ctypes.byref(native.cfg_struct(k2, t2i)), ctypes.byref(h)))
+
+
+def test_no_inflight_load_register_touched_before_its_wait():
+    """in the SHIPPED code object (libpdm.so's gfx950 bundles, disassembled), no instruction on any
+    control-flow path from a vector-memory load to its first vmcnt wait reads or writes the load's destination VGPRs
+    -- the guard for the attention kernels' inline-asm Q loads, whose waits hipcc does not know about
+    (tools/check_asm_loads.py; attention.hip PDM_WAIT_Q)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(repo, "panopticdiffusionmodels_amd", "libpdm.so")
+    if not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump") or not os.path.exists(lib):
+        pytest.skip("llvm-objdump or libpdm.so missing")
+    r = subprocess.run([sys.executable, os.path.join(repo, "tools", "check_asm_loads.py"), lib],
+                       capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    m = re.search(r"checked (\d+) VGPR-destination VMEM loads in (\d+) kernels \((\d+) plain", r.stdout)
+    assert m and int(m.group(1)) > 1000 and int(m.group(3)) > 0   # the walk saw the attention kernels' asm loads

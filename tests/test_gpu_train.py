@@ -251,6 +251,20 @@ def test_train_label_out_of_range_raises():
     for bad in (nc, -1):
         with pytest.raises(IndexError):
             st.forward_backward(xt, t, torch.tensor([0, bad]), eps)
+    # device-resident labels: clamped on the stream (no read outside label_emb), the error raised without a per-step
+    # synchronisation -- by check_labels(), or by the next step once the offending one has finished
+    loss = st.forward_backward(xt, t, torch.tensor([0, nc + 3]).cuda(), eps)
+    assert torch.isfinite(loss).all()
+    with pytest.raises(IndexError):
+        st.check_labels()
+    st.check_labels()   # reported once
+    st.forward_backward(xt, t, torch.tensor([-2, 1]).cuda(), eps)
+    torch.cuda.synchronize()
+    with pytest.raises(IndexError):
+        st.forward_backward(xt, t, torch.tensor([0, 1]).cuda(), eps)
+    st.forward_backward(xt, t, torch.tensor([0, 1]).cuda(), eps)
+    st.check_labels()
+    st.G.zero_()
     st.lr_scheduler["warmup_steps"] = 4
     out = st.train_step(torch.randn(2, 4, 16, 16, generator=g), torch.tensor([1, nc - 1]))
     assert st.step == 1 and abs(out["lr"] - st.optimizer["lr"] * 0.25) < 1e-15
