@@ -1456,6 +1456,12 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
   constexpr int E = EPI == EPI_RES ? 17 : MXO ? 20 : 16;
   constexpr int ES = FP8 ? 1 : 2;   // operand bytes per element
   constexpr int RW = FP8 ? 9 : 8;   // ring VMEM ops a lane leaves in flight at a phase wait (FP8: + the scale piece)
+#ifndef PDM_G8S_SCHED
+#define PDM_G8S_SCHED 0
+#endif
+  // experimental refill orders (A/B builds, bf16 whole tiles): 2 = a load segment's refills issued before its fragment
+  // reads, 3 = W1 of K-tile g+2 moved from phase B of g to phase A of g+1 (4 + 4 pieces per K-tile instead of 2 + 6)
+  constexpr int XS = (!FP8 && !SK) ? PDM_G8S_SCHED : 0;
   typedef int v8i __attribute__((ext_vector_type(8)));
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1616,8 +1622,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
         dma16(make_rsrc(v.ln_colsum + n0_, (long long)(p.N - n0_) * 4), (unsigned)(lane * 16), 0,
               (PDM_LDS void*)(smem + S_COL + 1024));
     }
-    if (wave == 6 && p.bias)
-      dma16(make_rsrc(v.bias + n0_, (long long)(p.N - n0_) * 4), (unsigned)(lane * 16), 0, (PDM_LDS void*)(smem + S_COL));
+    if (wave == 6)   // no bias: an empty descriptor stages zeros, so the epilogues add it unconditionally
+      dma16(v.bias ? make_rsrc(v.bias + n0_, (long long)(p.N - n0_) * 4) : make_rsrc(p.W, 0), (unsigned)(lane * 16), 0,
+            (PDM_LDS void*)(smem + S_COL));
   };
 
   bf16x8 af[4][2];
@@ -1739,6 +1746,11 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
   wait_vmcnt_n<RW>();
   bar_raw();
 
+#ifdef PDM_G8S_CLK
+  // diagnostic builds only: the in-kernel clock (shader-clock ticks / 100 MHz real-time ticks, summed over workgroups
+  // into g_sk_stats[0..2], read by pdm_gemm_sk_stats; MI355X_MICROARCH DVFS item 6; tools/g8s_clock.py)
+  const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   int g = 0;                  // K-steps run so far: the ring slot of the next one is g & 1
   bool pub_pending = false;   // SK: this workgroup's head slab stored, its flag not yet raised
   // Ordering of the hand-off (relaxed atomics by design): publish() runs only after EVERY wave of this
@@ -1828,25 +1840,96 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       }
     }
     if (wave >= 4) bar_raw();        // stagger: waves 4-7 one barrier behind
+#ifdef PDM_G8S_DIAG
+    // diagnostic builds only (tools/build_variant.sh TAG -DPDM_G8S_DIAG=bits, tools/g8s_diag.py): bits 1 / 2 / 4 drop
+    // the main loop's LDS-DMA refills / fragment reads / MFMAs (wrong results; timing of what bounds the loop)
+    constexpr bool d_nodma = PDM_G8S_DIAG & 1, d_noread = PDM_G8S_DIAG & 2, d_nomma = PDM_G8S_DIAG & 4;
+#else
+    constexpr bool d_nodma = false, d_noread = false, d_nomma = false;
+#endif
     for (int kt = kb; kt < ke; ++kt, ++g) {
       const int slot = g & 1;
       const char* buf = smem + slot * BUF;
       const bool first = kt == kb && after_epi;
       const bool m1 = kt + 1 < ke || has_next;   // K-tile g+1 exists (this segment's kt+1 or the next one's kbn)
       const bool m2 = kt + 2 < ke || has_next;   // K-tile g+2 (segments >= 2 K-tiles: the next one's kbn + {0, 1})
+      if constexpr (XS == 2 || XS == 3) {
+        const int k1 = kt + 1 < ke ? kt + 1 : kbn;
+        const int k2 = kt + 2 < ke ? kt + 2 : kbn + (kt + 2 - ke);
+        // XS 3: phase A issues W1(g+1) (moved from phase B of g-1; the prologue / the previous segment's last K-tiles
+        // still issue it there) and A1(g+1)
+        const bool w1 = XS == 3 && m1 && kt + 1 < ke && kt > kb;
+        if constexpr (XS == 2) {
+          if (m1) issue(slot ^ 1, k1, KA1);
+        }
+        read_a(buf, 0);
+        read_w(buf, 0);
+        read_w(buf, 1);
+        lds_done();
+        if constexpr (XS == 3) {
+          if (w1) issue(slot ^ 1, k1, KW1);
+          if (m1) issue(slot ^ 1, k1, KA1);
+        }
+        // retire A1(g); younger: A0 W0 W1 (g+1), A1(g+1) (+ the epilogue's E stores)
+        if (!m1) wait_vmcnt_n<0>();
+        else if (first) wait_vmcnt_n<8 + E>();
+        else wait_vmcnt_n<8>();
+        bar_raw();
+        mma(0, 0);
+        mma(0, 1);
+        bar_raw();
+        if (kt == ke - 2 && has_next) set_tile(nv, m0n, n0n);
+        // XS 3: W1(g+2) stays here when g+2 is the first K-tile of its segment or its segment's second (the next
+        // phase A belongs to the previous tile / the first K-tile's phase A has no W1 to issue)
+        const bool w1b = XS == 2 || !(kt + 2 < ke && kt + 1 > kb);
+        if constexpr (XS == 2) {
+          if (m2) {
+            issue(slot, k2, KA0);
+            issue(slot, k2, KW0);
+            issue(slot, k2, KW1);
+          }
+        }
+        read_a(buf, 1);
+        lds_done();
+        if constexpr (XS == 3) {
+          if (m2) {
+            issue(slot, k2, KA0);
+            issue(slot, k2, KW0);
+            if (w1b) issue(slot, k2, KW1);
+          }
+        }
+        // retire A0 W0 W1(g+1); younger: A1(g+1), A0 W0 (W1) (g+2)
+        if (m2) {
+          const bool w1n = XS == 2 || w1b;   // W1(g+2) issued in this phase
+          if (first) {
+            if (w1n) wait_vmcnt_n<8 + E>();
+            else wait_vmcnt_n<6 + E>();
+          } else {
+            if (w1n) wait_vmcnt_n<8>();
+            else wait_vmcnt_n<6>();
+          }
+        } else if (m1) {
+          wait_vmcnt_n<2>();
+        }
+        bar_raw();
+        mma(1, 0);
+        mma(1, 1);
+        bar_raw();
+        continue;
+      }
       // phase A: quadrants (0,0) (0,1); issues A1 of K-tile g+1
       if constexpr (FP8) {
         read_a8(buf, 0);
         read_w8(buf);
         read_scales(slot);
-      } else {
+      } else if (!d_noread) {
         read_a(buf, 0);
         read_w(buf, 0);
         read_w(buf, 1);
       }
       lds_done();
       if (m1) {
-        issue(slot ^ 1, kt + 1 < ke ? kt + 1 : kbn, KA1);
+        if (!d_nodma) issue(slot ^ 1, kt + 1 < ke ? kt + 1 : kbn, KA1);
         if (first && after_slab) wait_vmcnt_n<8 + 32>();
         else if (first) wait_vmcnt_n<RW + E>();
         else wait_vmcnt_n<RW>();
@@ -1857,22 +1940,24 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       if constexpr (FP8) {
         mma8(I0{}, I0{});
         mma8(I0{}, I1{});
-      } else {
+      } else if (!d_nomma) {
         mma(0, 0);
         mma(0, 1);
       }
       bar_raw();
       // phase B: quadrants (1,0) (1,1); issues A0 W0 W1 of K-tile g+2 (the next segment's from kt = ke-2 on)
       if constexpr (FP8) read_a8(buf, 1);
-      else read_a(buf, 1);
+      else if (!d_noread) read_a(buf, 1);
       lds_done();
       if (kt == ke - 2 && has_next) set_tile(nv, m0n, n0n);
       if (m2) {
         const int k2 = kt + 2 < ke ? kt + 2 : kbn + (kt + 2 - ke);
         issue_scales(slot, k2);
-        issue(slot, k2, KA0);
-        issue(slot, k2, KW0);
-        issue(slot, k2, KW1);
+        if (!d_nodma) {
+          issue(slot, k2, KA0);
+          issue(slot, k2, KW0);
+          issue(slot, k2, KW1);
+        }
         if (first && after_slab) wait_vmcnt_n<8 + 32>();
         else if (first) wait_vmcnt_n<RW + E>();
         else wait_vmcnt_n<RW>();
@@ -1888,7 +1973,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       if constexpr (FP8) {
         mma8(I1{}, I0{});
         mma8(I1{}, I1{});
-      } else {
+      } else if (!d_nomma) {
         mma(1, 0);
         mma(1, 1);
       }
@@ -1971,7 +2056,6 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
     for (int qj = 0; qj < 2; ++qj)
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
-        if (!p.bias) bv[qj][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (!ln || lnc) cs[qj][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     bar_raw();   // lnrow complete; the raw / column tables are free for the next tile's
@@ -2102,18 +2186,22 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
         }
       }
     } else {   // EPI_RES
-      // residual rows in the 16-byte layout (zeros out of range), all issued before the first use
+      // Residual rows in the 16-byte layout, all issued before the first use.  No per-value masks: rows past M fall
+      // past the descriptors' num_records (the hardware reads zeros and drops the stores), and a column past N holds
+      // exactly 0 (zero W rows, zero-staged bias, a masked residual load), so it adds nothing to a row's sum and
+      // (0 - mu)^2 to its M2, which is subtracted per row below.  Only the column test stays on each 16-byte access.
       i32x4 rr[2][4][2];
       const bool acc_res = p.accumulate != 0;
+      const bool drop_st = p.dbg_tile0 & 32, drop_res = !acc_res || (p.dbg_tile0 & 64);
 #pragma unroll
       for (int qi = 0; qi < 2; ++qi)
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
           for (int qj = 0; qj < 2; ++qj) {
-            const int m = m0 + qi * 128 + wm * 64 + mi * 16 + r16, n = n0 + qj * 128 + wn * 32 + offg;
-            const unsigned off = (acc_res && m < M && n < p.N && !(p.dbg_tile0 & 64))
-                                     ? ((unsigned)m * (unsigned)p.ldri + (unsigned)n) * 2u : OOB;
+            const unsigned m = (unsigned)(m0 + qi * 128 + wm * 64 + mi * 16 + r16);
+            const int n = n0 + qj * 128 + wn * 32 + offg;
+            const unsigned off = (!drop_res && n < p.N) ? (m * (unsigned)p.ldri + (unsigned)n) * 2u : OOB;
             rr[qi][mi][qj] = __builtin_amdgcn_raw_buffer_load_b128(rres, (int)off, 0, 0);
           }
       const int ncols = min(256, p.N - n0);
@@ -2122,9 +2210,8 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       for (int qi = 0; qi < 2; ++qi)
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) {
-          const int ml = qi * 128 + wm * 64 + mi * 16 + r16;
-          const int m = m0 + ml;
-          float s = 0.f;
+          const unsigned m = (unsigned)(m0 + qi * 128 + wm * 64 + mi * 16 + r16);
+          f32x2 s2 = f32x2{0.f, 0.f};
 #pragma unroll
           for (int qj = 0; qj < 2; ++qj) {
             unsigned r0 = (unsigned)rr[qi][mi][qj][0], r1 = (unsigned)rr[qi][mi][qj][1];
@@ -2137,24 +2224,22 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
             for (int ni = 0; ni < 2; ++ni) {
               f32x4& v = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
               v += bv[qj][ni];
-              v[0] += bf16lo(rs[ni][0]); v[1] += bf16hi(rs[ni][0]);
-              v[2] += bf16lo(rs[ni][1]); v[3] += bf16hi(rs[ni][1]);
+              v += f32x4{bf16lo(rs[ni][0]), bf16hi(rs[ni][0]), bf16lo(rs[ni][1]), bf16hi(rs[ni][1])};
               u[ni][0] = pack_bf16x2(v[0], v[1]);
               u[ni][1] = pack_bf16x2(v[2], v[3]);
-              // the rounded values feed the partials (exactly what the next GEMM reads); columns past N are 0
-              const bool valid = qj * 128 + wn * 32 + ni * 16 + g4 * 4 < ncols;
-              v = valid ? f32x4{bf16lo(u[ni][0]), bf16hi(u[ni][0]), bf16lo(u[ni][1]), bf16hi(u[ni][1])}
-                        : f32x4{0.f, 0.f, 0.f, 0.f};
-              s += (v[0] + v[1]) + (v[2] + v[3]);
+              // the rounded values feed the partials (exactly what the next GEMM reads)
+              v = f32x4{bf16lo(u[ni][0]), bf16hi(u[ni][0]), bf16lo(u[ni][1]), bf16hi(u[ni][1])};
+              s2 += f32x2{v[0], v[1]};
+              s2 += f32x2{v[2], v[3]};
             }
             pl16swap(u[0][0], u[1][0]);
             pl16swap(u[0][1], u[1][1]);
             const int n = n0 + qj * 128 + wn * 32 + offg;
-            const unsigned off = (m < M && n < p.N && !(p.dbg_tile0 & 32)) ? ((unsigned)m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
+            const unsigned off = (!drop_st && n < p.N) ? (m * (unsigned)p.ldo + (unsigned)n) * 2u : OOB;
             __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)u[0][0], (int)u[0][1], (int)u[1][0], (int)u[1][1]},
                                                    rout, (int)off, 0, 0);
           }
-          rsum[qi][mi] = s;
+          rsum[qi][mi] = s2[0] + s2[1];
         }
       // LayerNorm partials of the 256-column group (sum, M2 about the group mean): every wave reduces its own 64
       // columns of a row (sum over the 4 lane rows, M2 about the wave's own mean) and the 4 column waves (wn) are
@@ -2165,23 +2250,24 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       if (stats) {
         const int nw = wave_cols(wn);
         const float inv_w = nw > 0 ? 1.0f / (float)nw : 0.f;
+        const float nzero = (float)(64 - nw);   // the wave's columns past N: exact zeros, (0 - mu)^2 each in q
 #pragma unroll
         for (int qi = 0; qi < 2; ++qi)
 #pragma unroll
           for (int mi = 0; mi < 4; ++mi) {
             const float sw = xrow_sum4(rsum[qi][mi]);
             const float mu = sw * inv_w;
-            float q = 0.f;
+            f32x2 q2 = f32x2{0.f, 0.f};
 #pragma unroll
             for (int qj = 0; qj < 2; ++qj)
 #pragma unroll
               for (int ni = 0; ni < 2; ++ni) {
-                const f32x4 d = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi] - mu;
-                const bool valid = qj * 128 + wn * 32 + ni * 16 + g4 * 4 < ncols;
-                const float dq = (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
-                q += valid ? dq : 0.f;
+                const f32x4 a = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
+                const f32x2 d0 = f32x2{a[0], a[1]} - mu, d1 = f32x2{a[2], a[3]} - mu;
+                q2 += d0 * d0;
+                q2 += d1 * d1;
               }
-            q = xrow_sum4(q);
+            const float q = xrow_sum4(q2[0] + q2[1]) - nzero * mu * mu;
             if (g4 == 0) lds_wr64(tab + ((qi * 128 + wm * 64 + mi * 16 + r16) * 4 + wn) * 8, make_float2(sw, q));
           }
       }
@@ -2215,6 +2301,14 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
     kind = kindn;
     if constexpr (GRP) cv = nv;
   }
+#ifdef PDM_G8S_CLK
+  if (tid == 0) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(&g_sk_stats[0], t1 - clk_t0);
+    atomicAdd(&g_sk_stats[1], r1 - clk_r0);
+    atomicAdd(&g_sk_stats[2], 1ull);
+  }
+#endif
 }
 
 // the one-problem kernel keeps its own signature (a second by-value GemmArgs in every launch measured +0.7 % on the

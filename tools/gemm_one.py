@@ -1,5 +1,5 @@
 """Run one GEMM shape repeatedly (profiling target): python tools/gemm_one.py ALGO M N K EPI [ITERS]
-(env PDM_RASTER: tile-order raster, pdm_set_gemm_tuning; 1 = row-major)"""
+(env PDM_RASTER: tile-order raster, pdm_set_gemm_tuning; 1 = row-major; PDM_DBG: its timing bits, e.g. 16 = no epilogue)"""
 import os
 import sys
 
@@ -12,8 +12,9 @@ algo, M, N, K, epi = (int(v) for v in sys.argv[1:6])
 iters = int(sys.argv[6]) if len(sys.argv) > 6 else 20
 lib = _lib.load()
 assert lib.pdm_set_gemm_algo(algo) == 0, lib.pdm_last_error()
-if os.environ.get("PDM_RASTER"):
-    assert lib.pdm_set_gemm_tuning(int(os.environ["PDM_RASTER"]), 0) == 0, lib.pdm_last_error()
+if os.environ.get("PDM_RASTER") or os.environ.get("PDM_DBG"):
+    assert lib.pdm_set_gemm_tuning(int(os.environ.get("PDM_RASTER", "0")), int(os.environ.get("PDM_DBG", "0"))) == 0, \
+        lib.pdm_last_error()
 g = torch.Generator(device="cuda").manual_seed(0)
 a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
 w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
