@@ -1444,7 +1444,8 @@ __device__ __forceinline__ TV tile_view(const GemmArgs& p, const TV& t2, bool se
 template <int EPI, int MXO, int GRP, int SK = 0, int FP8 = 0>
 __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int ntiles, const TV& p2, int nt0) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_RES, "persistent kernel epilogues");
-  static_assert(!FP8 || (EPI == EPI_BF16 && !MXO && !GRP && !SK), "MXFP8 operands: one-problem bf16 epilogue");
+  static_assert(!FP8 || ((EPI == EPI_BF16 || EPI == EPI_RES) && !MXO && !GRP && !SK),
+                "MXFP8 operands: one problem, the bf16 or the bf16-residual epilogue");
   static_assert(!MXO || EPI != EPI_RES, "MXFP8 output: bf16 / GELU epilogues");
   static_assert(!SK || !GRP, "stream-K: one problem");
   constexpr int ROWB = 128;
@@ -2886,6 +2887,12 @@ const char* gemm_check(const GemmArgs& p, int epi) {
 }
 
 static int g_gemm_algo = 0;
+// the MXFP8 residual GEMM (H/4 proj) on the persistent kernel under the automatic policy (an A/B build sets
+// -DPDM_MX_RES_PERSIST=0 for gemm_mx_kernel<EPI_RES>)
+#ifndef PDM_MX_RES_PERSIST
+#define PDM_MX_RES_PERSIST 1
+#endif
+static bool g_mx_res_persist = PDM_MX_RES_PERSIST;
 static int g_gemm_sk = 0;   // off by default: measured slower at every U-ViT shape (profiles/r05a, r05b)
 static long long g_sk_launches = 0;   // stream-K launches so far (host count, tests)
 void gemm_set_sk(int mode) { g_gemm_sk = mode; }
@@ -3107,7 +3114,8 @@ static bool persist_kernels_ok() {
                          (const void*)gemm8s_kernel<EPI_GELU, 0, 1>, (const void*)gemm8s_kernel<EPI_RES, 0, 1>,
                          (const void*)gemm8s_kernel<EPI_BF16, 1, 1>, (const void*)gemm8s_kernel<EPI_GELU, 1, 1>,
                          (const void*)gemm8g_kernel<EPI_BF16>, (const void*)gemm8g_kernel<EPI_GELU>,
-                         (const void*)gemm8g_kernel<EPI_RES>, (const void*)gemm8s_kernel<EPI_BF16, 0, 0, 1>};
+                         (const void*)gemm8g_kernel<EPI_RES>, (const void*)gemm8s_kernel<EPI_BF16, 0, 0, 1>,
+                         (const void*)gemm8s_kernel<EPI_RES, 0, 0, 1>};
     ok = 1;
     for (const void* f : fns) {
       hipFuncAttributes at{};
@@ -3143,23 +3151,30 @@ static bool fits_8s(const GemmArgs& p, int epi) {
   return fits_rsrc(p);
 }
 
-// the persistent kernel's MXFP8-operand form (gemm8s_kernel<EPI_BF16, 0, 0, 1>, algo 11 only): the bf16 epilogue with
-// or without the (centred) LayerNorm consumer -- the U-ViT-H/4 qkv; everything else keeps gemm_mx_kernel
+// the persistent kernel's MXFP8-operand form (gemm8s_kernel<EPI, 0, 0, 1>): the bf16 epilogue with or without the
+// (centred) LayerNorm consumer -- the U-ViT-H/4 qkv, algo 11 only -- and the bf16-residual epilogue without an MXFP8
+// output copy -- the H/4 proj in 'fp8' mode (its x feeds the bf16 fc1), automatic where g_mx_res_persist allows
 static bool fits_8s_mx(const GemmArgs& p, int epi) {
   const long long lim = 0x7fffffffLL;
   if (!persist_kernels_ok()) return false;
-  if (epi != EPI_BF16 || !p.fp8 || p.out_fp8 || p.A2 || p.K1 != p.K || p.conv || p.batch > 1 || p.a_rows_per_group > 0)
+  if ((epi != EPI_BF16 && epi != EPI_RES) || !p.fp8 || p.out_fp8 || p.mx_center || p.A2 || p.K1 != p.K || p.conv ||
+      p.batch > 1 || p.a_rows_per_group > 0 || p.out2)
     return false;
   if (!p.out_bf16 || p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15) || p.K % 128 || p.K < 512) return false;
   if (p.ln_stats && p.ln_ld > 8) return false;
   if ((long long)p.M * p.ldo * 2 >= lim || (p.dbg_tile0 & 15)) return false;
+  if (epi == EPI_RES && p.accumulate && (p.ldri % 8 || ((uintptr_t)p.res_in & 15) || (long long)p.M * p.ldri * 2 >= lim))
+    return false;
+  if (p.stats_out && (long long)p.M * p.stats_ld * 8 >= lim) return false;
   return fits_rsrc(p);
 }
 
-static hipError_t launch8s_mx(const GemmArgs& p, hipStream_t stream) {
+static hipError_t launch8s_mx(const GemmArgs& p, int epi, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 0, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              S_SMEM_MX);
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_RES, 0, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               S_SMEM_MX);
     attr_set = true;
   }
@@ -3170,7 +3185,10 @@ static hipError_t launch8s_mx(const GemmArgs& p, hipStream_t stream) {
   const int tn = (p.N + BN2 - 1) / BN2, tm = (p.M + BM2 - 1) / BM2;
   const int ntiles = tm * tn;
   const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
-  hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 0, 0, 1>), dim3(grid), dim3(512), S_SMEM_MX, stream, p, tn, ntiles);
+  if (epi == EPI_RES)
+    hipLaunchKernelGGL((gemm8s_kernel<EPI_RES, 0, 0, 1>), dim3(grid), dim3(512), S_SMEM_MX, stream, p, tn, ntiles);
+  else
+    hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 0, 0, 1>), dim3(grid), dim3(512), S_SMEM_MX, stream, p, tn, ntiles);
   return hipGetLastError();
 }
 
@@ -3270,7 +3288,11 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
     if (!fits_rsrc(p)) return hipErrorInvalidValue;
     // the persistent form on request only (algo 11): measured 3.5-4.7 % slower than gemm_mx_kernel on the H/4 qkv
     // at 50-190 rows (tools/mx_qkv_bench.py), so the automatic choice stays one tile per workgroup
-    if (g_gemm_algo == 11 && fits_8s_mx(p, epi)) return launch8s_mx(p, stream);
+    // the persistent residual form from 64 sequences of 258 tokens up: H/4 proj at 100 rows 64.3 -> 60.6 us, at the
+    // bench's 50-row lanes 36.4 vs 36.8 us (tools/mx_res_bench.py, profiles/r06j); outputs bit-identical
+    if ((g_gemm_algo == 11 || (g_gemm_algo == 0 && epi == EPI_RES && g_mx_res_persist && p.M >= 16384)) &&
+        fits_8s_mx(p, epi))
+      return launch8s_mx(p, epi, stream);
     return launch_mx(p, epi, stream);
   }
   if (p.out_fp8) algo = 7;   // MXFP8 output lives in the 256-tile epilogue

@@ -167,6 +167,36 @@ def test_mx_persistent_vs_tile_kernel(lib, M, N, K, centred):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("M,N,K", [(25800, 1152, 1152), (16400, 1152, 1152), (4133, 1152, 1152), (20000, 520, 1152)])
+def test_mx_persistent_residual_vs_tile_kernel(lib, M, N, K):
+    """The MXFP8 residual GEMM (the H/4 proj: bf16 residual in place + LayerNorm partials) on the persistent kernel
+    (gemm8s_kernel<EPI_RES, 0, 0, 1>: algo 11, and automatic from 16,384 rows) against gemm_mx_kernel<EPI_RES> (algo 7):
+    the output bit-identical ((acc + bias) + residual rounded once in both), the partials within 1e-5 (summation
+    order), and against float64 torch.  Ragged M, N = 1152 (a 128-wide last column tile) and N = 520."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + 5)
+    qa, sa, _ = _mx(lib, torch.randn(M, K, device="cuda", generator=g))
+    qw, sw, _ = _mx(lib, torch.randn(N, K, device="cuda", generator=g) * K ** -0.5)
+    bias = torch.randn(N, device="cuda", generator=g)
+    res0 = (torch.randn(M, N, device="cuda", generator=g) * 3 + 2).bfloat16()
+    outs = {}
+    try:
+        for algo in (7, 11, 0):
+            lib.check(lib.load().pdm_set_gemm_algo(algo), "pdm_set_gemm_algo")
+            out = res0.clone()
+            st = torch.full((M, (N + 255) // 256, 2), float("nan"), device="cuda")
+            lib.gemm_ex(lib.EPI_RES, qa, qw, bias, sa, sw, out=out, res_in=out, accumulate=True, stats_out=st)
+            outs[algo] = (out, st)
+    finally:
+        lib.load().pdm_set_gemm_algo(0)
+    for algo in (11, 0):
+        assert torch.equal(outs[algo][0], outs[7][0])
+        assert rel(outs[algo][1], outs[7][1]) < 1e-5
+    x = outs[11][0].double()
+    grp = [x[:, t * 256:(t + 1) * 256] for t in range((N + 255) // 256)]
+    ref = torch.stack([torch.stack([c.sum(1), ((c - c.mean(1, keepdim=True)) ** 2).sum(1)], -1) for c in grp], 1)
+    assert rel(outs[11][1].double(), ref) < 1e-5
+
+
 @pytest.mark.parametrize("centred,offset", [(False, 0.0), (True, 0.0), (True, 2.0), (True, 8.0), (True, 32.0)])
 def test_mxfp8_layernorm_consumer_chain(lib, centred, offset):
     """fc1 of a U-ViT-H block in fp8: MX(x) operand + gamma-folded MX weight + fused LayerNorm + GELU, emitting
