@@ -59,13 +59,19 @@ int pdm_set_gemm_algo(int algo);
 /* stream-K policy of the persistent GEMM (the last, partly filled wave of 256 x 256 tiles spread over all CUs as
  * K-step ranges; results bit-identical to whole tiles): 0 off (default: measured slower at every U-ViT shape,
  * DESIGN.md §4c), 1 auto (where the last wave is < 97 % full), 2 wherever it applies; + 4: standalone pdm_gemm calls
- * take it too, on library-owned state (one stream at a time; the forwards use their workspace's own state) */
+ * take it too.  The flag blocks and the 64 MiB fp32 slab are library-owned, one set per (device, stream), allocated
+ * on first use outside a stream capture (a forward captured without one keeps whole tiles) */
 int pdm_set_gemm_sk(int mode);
 /* number of stream-K GEMM launches issued by this process so far (host-side count) */
 long long pdm_gemm_sk_launches(void);
 /* stream-K diagnostics gathered while pdm_set_gemm_tuning bit 8 is set: out3 = {tails run, hand-offs not taken,
  * summed poll time in 10 ns ticks}; reading clears them (synchronises the device) */
 int pdm_gemm_sk_stats(unsigned long long* out3);
+/* diagnostics of -DPDM_G8S_SEG builds (tools/g8s_seg.py): shader cycles per persistent-GEMM main-loop segment summed
+ * over workgroups -- wave 0 [0..7] and wave 4 [8..15] (load A, barrier, MFMA A, barrier, load B, barrier, MFMA B,
+ * barrier) -- and the workgroup count [16]; reading clears them.  Zeros in production builds (a measurement hook with
+ * no reference counterpart) */
+int pdm_gemm_seg_stats(unsigned long long* out17);
 int pdm_set_attention_algo(int algo);
 
 /* ---- network handle: libs/uvit.py:138-230 UViT, libs/uvit_t2i.py:258-525 UViT (t2i) -------------- */

@@ -80,6 +80,7 @@ _SIGS = {
     "pdm_set_gemm_sk": (ctypes.c_int, [ctypes.c_int]),
     "pdm_gemm_sk_launches": (ctypes.c_longlong, []),
     "pdm_gemm_sk_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
+    "pdm_gemm_seg_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     "pdm_set_attention_algo": (ctypes.c_int, [ctypes.c_int]),
     "pdm_set_gemm_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "pdm_uvit_create": (ctypes.c_int, [ctypes.POINTER(PdmUvitCfg), ctypes.POINTER(ctypes.c_void_p)]),

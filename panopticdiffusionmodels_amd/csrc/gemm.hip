@@ -1356,6 +1356,9 @@ __device__ __forceinline__ void lds_rd_rowc(const void* p, i32x4 (&v)[8]) {
 }
 // stream-K diagnostics (pdm_set_gemm_tuning bit 8): tails run, hand-offs not taken, summed poll time
 __device__ unsigned long long g_sk_stats[4];
+// -DPDM_G8S_SEG diagnostic builds: shader cycles per main-loop segment, summed over workgroups for wave 0 [0..7] and
+// wave 4 [8..15] (load A, barrier, MFMA A, barrier, load B, barrier, MFMA B, barrier) + launches [16]
+__device__ unsigned long long g_seg_stats[17];
 
 // a copy of x the compiler cannot see through: values derived from it are computed where they are used instead of
 // being hoisted and held in registers across loops
@@ -1753,6 +1756,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
   const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
   int g = 0;                  // K-steps run so far: the ring slot of the next one is g & 1
+#ifdef PDM_G8S_SEG
+  unsigned seg_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
   bool pub_pending = false;   // SK: this workgroup's head slab stored, its flag not yet raised
   // Ordering of the hand-off (relaxed atomics by design): publish() runs only after EVERY wave of this
   // workgroup has drained its slab stores (wait_vmcnt_n<0> + barrier in the tail branch below; the stores are sc1
@@ -1848,6 +1854,16 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
 #else
     constexpr bool d_nodma = false, d_noread = false, d_nomma = false;
 #endif
+#ifdef PDM_G8S_SEG
+    unsigned long long seg_t = __builtin_amdgcn_s_memtime();
+    auto seg = [&](int i) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      seg_acc[i] += (unsigned)(t - seg_t);
+      seg_t = t;
+    };
+#else
+    auto seg = [](int) {};
+#endif
     for (int kt = kb; kt < ke; ++kt, ++g) {
       const int slot = g & 1;
       const char* buf = smem + slot * BUF;
@@ -1937,7 +1953,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       } else {
         wait_vmcnt_n<0>();
       }
+      seg(0);
       bar_raw();
+      seg(1);
       if constexpr (FP8) {
         mma8(I0{}, I0{});
         mma8(I0{}, I1{});
@@ -1945,7 +1963,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
         mma(0, 0);
         mma(0, 1);
       }
+      seg(2);
       bar_raw();
+      seg(3);
       // phase B: quadrants (1,0) (1,1); issues A0 W0 W1 of K-tile g+2 (the next segment's from kt = ke-2 on)
       if constexpr (FP8) read_a8(buf, 1);
       else if (!d_noread) read_a(buf, 1);
@@ -1965,7 +1985,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       } else if (m1) {
         wait_vmcnt_n<2>();
       }
+      seg(4);
       bar_raw();
+      seg(5);
       // SK: the head slab's stores are older than everything this K-tile's phase-A wait left in flight, and by this
       // barrier every wave (4-7 one barrier behind) has passed that wait: raise the flag
       if constexpr (SK) {
@@ -1978,7 +2000,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
         mma(1, 0);
         mma(1, 1);
       }
+      seg(6);
       bar_raw();
+      seg(7);
     }
     if (wave < 4) bar_raw();   // rejoin the stagger
 
@@ -2302,6 +2326,13 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
     kind = kindn;
     if constexpr (GRP) cv = nv;
   }
+#ifdef PDM_G8S_SEG
+  if (lane == 0 && (wave == 0 || wave == 4)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_seg_stats[(wave == 4 ? 8 : 0) + i], (unsigned long long)seg_acc[i]);
+    if (wave == 0) atomicAdd(&g_seg_stats[16], 1ull);
+  }
+#endif
 #ifdef PDM_G8S_CLK
   if (tid == 0) {
     const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -2898,6 +2929,12 @@ static long long g_sk_launches = 0;   // stream-K launches so far (host count, t
 void gemm_set_sk(int mode) { g_gemm_sk = mode; }
 int gemm_get_sk() { return g_gemm_sk; }
 long long gemm_sk_launches() { return g_sk_launches; }
+int gemm_seg_stats(unsigned long long* out) {   // reads and clears the -DPDM_G8S_SEG counters (17; synchronises)
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg_stats), 17 * sizeof(unsigned long long)) != hipSuccess) return 1;
+  unsigned long long z[17] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_seg_stats), z, sizeof(z)) != hipSuccess;
+}
 int gemm_sk_stats(unsigned long long* out) {   // reads and clears the device counters (synchronises the device)
   if (hipDeviceSynchronize() != hipSuccess) return 1;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sk_stats), 3 * sizeof(unsigned long long)) != hipSuccess) return 1;
