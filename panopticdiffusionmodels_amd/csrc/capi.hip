@@ -966,9 +966,9 @@ int pdm_set_gemm_sk(int mode) {
 
 long long pdm_gemm_sk_launches(void) { return pdm::gemm_sk_launches(); }
 
-int pdm_gemm_seg_stats(unsigned long long* out17) {
-  if (!out17) return fail(PDM_ERR_ARG, "pdm_gemm_seg_stats: null output");
-  if (pdm::gemm_seg_stats(out17)) return fail(PDM_ERR_HIP, "pdm_gemm_seg_stats: device copy failed");
+int pdm_gemm_seg_stats(unsigned long long* out25) {
+  if (!out25) return fail(PDM_ERR_ARG, "pdm_gemm_seg_stats: null output");
+  if (pdm::gemm_seg_stats(out25)) return fail(PDM_ERR_HIP, "pdm_gemm_seg_stats: device copy failed");
   return PDM_OK;
 }
 int pdm_gemm_sk_stats(unsigned long long* out3) {

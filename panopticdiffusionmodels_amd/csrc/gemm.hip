@@ -1356,9 +1356,9 @@ __device__ __forceinline__ void lds_rd_rowc(const void* p, i32x4 (&v)[8]) {
 }
 // stream-K diagnostics (pdm_set_gemm_tuning bit 8): tails run, hand-offs not taken, summed poll time
 __device__ unsigned long long g_sk_stats[4];
-// -DPDM_G8S_SEG diagnostic builds: shader cycles per main-loop segment, summed over workgroups for wave 0 [0..7] and
-// wave 4 [8..15] (load A, barrier, MFMA A, barrier, load B, barrier, MFMA B, barrier) + launches [16]
-__device__ unsigned long long g_seg_stats[17];
+// -DPDM_G8S_SEG diagnostic builds: shader cycles per main-loop segment, summed over workgroups for wave 0 [0..11] and
+// wave 4 [12..23] (A: reads, refill issue, vmcnt wait, barrier, MFMAs, barrier; B: the same) + workgroups [24]
+__device__ unsigned long long g_seg_stats[25];
 
 // a copy of x the compiler cannot see through: values derived from it are computed where they are used instead of
 // being hoisted and held in registers across loops
@@ -1444,7 +1444,10 @@ __device__ __forceinline__ TV tile_view(const GemmArgs& p, const TV& t2, bool se
 // (waves 0-3: the tile's A rows, 4-7: its W rows) issued with A0 W0 W1, so the ring waits count 9 ops instead of 8.
 // bf16 epilogue only, with the centred LayerNorm consumer (ln_gcol: acc += sum_t (mu_t - mean) c_t as one bf16 MFMA
 // per accumulator, as gemm_mx_kernel) or the plain one: the U-ViT-H/4 qkv.
-template <int EPI, int MXO, int GRP, int SK = 0, int FP8 = 0>
+// DUAL = 0: no split-K second A operand (A2 / K1 < K: the long-skip concat of skip_linear only): the refill issue then
+// has no per-piece operand test and descriptor select -- measured 4-7 % on the single-operand Linears at 50 rows
+// (profiles/r06n: proj 39.5 -> 37.8, fc1 131.7 -> 123.7, fc2 99.2 -> 94.8 us), whose load segments are issue-bound
+template <int EPI, int MXO, int GRP, int SK = 0, int FP8 = 0, int DUAL = 1>
 __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int ntiles, const TV& p2, int nt0) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_RES, "persistent kernel epilogues");
   static_assert(!FP8 || ((EPI == EPI_BF16 || EPI == EPI_RES) && !MXO && !GRP && !SK),
@@ -1597,7 +1600,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
     for (int i = 0; i < 2; ++i) {
       PDM_LDS void* d = (PDM_LDS void*)(dst + (wave * 2 + i) * 1024);
       if (kind >= KW0) dma16(rw, woff[kind - KW0][i], k0 * 2, d);
-      else if (k0 < p.K1) dma16(ra1, aoff[kind][i], k0 * 2, d);
+      else if (!DUAL || k0 < p.K1) dma16(ra1, aoff[kind][i], k0 * 2, d);
       else dma16(ra2, aoff[kind][i], (k0 - p.K1) * 2, d);
     }
   };
@@ -1757,7 +1760,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
 #endif
   int g = 0;                  // K-steps run so far: the ring slot of the next one is g & 1
 #ifdef PDM_G8S_SEG
-  unsigned seg_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned seg_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   bool pub_pending = false;   // SK: this workgroup's head slab stored, its flag not yet raised
   // Ordering of the hand-off (relaxed atomics by design): publish() runs only after EVERY wave of this
@@ -1945,17 +1948,19 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
         read_w(buf, 1);
       }
       lds_done();
+      seg(0);
       if (m1) {
         if (!d_nodma) issue(slot ^ 1, kt + 1 < ke ? kt + 1 : kbn, KA1);
+        seg(1);
         if (first && after_slab) wait_vmcnt_n<8 + 32>();
         else if (first) wait_vmcnt_n<RW + E>();
         else wait_vmcnt_n<RW>();
       } else {
         wait_vmcnt_n<0>();
       }
-      seg(0);
+      seg(2);
       bar_raw();
-      seg(1);
+      seg(3);
       if constexpr (FP8) {
         mma8(I0{}, I0{});
         mma8(I0{}, I1{});
@@ -1963,13 +1968,14 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
         mma(0, 0);
         mma(0, 1);
       }
-      seg(2);
+      seg(4);
       bar_raw();
-      seg(3);
+      seg(5);
       // phase B: quadrants (1,0) (1,1); issues A0 W0 W1 of K-tile g+2 (the next segment's from kt = ke-2 on)
       if constexpr (FP8) read_a8(buf, 1);
       else if (!d_noread) read_a(buf, 1);
       lds_done();
+      seg(6);
       if (kt == ke - 2 && has_next) set_tile(nv, m0n, n0n);
       if (m2) {
         const int k2 = kt + 2 < ke ? kt + 2 : kbn + (kt + 2 - ke);
@@ -1979,15 +1985,16 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
           issue(slot, k2, KW0);
           issue(slot, k2, KW1);
         }
+        seg(7);
         if (first && after_slab) wait_vmcnt_n<8 + 32>();
         else if (first) wait_vmcnt_n<RW + E>();
         else wait_vmcnt_n<RW>();
       } else if (m1) {
         wait_vmcnt_n<2>();
       }
-      seg(4);
+      seg(8);
       bar_raw();
-      seg(5);
+      seg(9);
       // SK: the head slab's stores are older than everything this K-tile's phase-A wait left in flight, and by this
       // barrier every wave (4-7 one barrier behind) has passed that wait: raise the flag
       if constexpr (SK) {
@@ -2000,9 +2007,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
         mma(1, 0);
         mma(1, 1);
       }
-      seg(6);
+      seg(10);
       bar_raw();
-      seg(7);
+      seg(11);
     }
     if (wave < 4) bar_raw();   // rejoin the stagger
 
@@ -2329,8 +2336,8 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
 #ifdef PDM_G8S_SEG
   if (lane == 0 && (wave == 0 || wave == 4)) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) atomicAdd(&g_seg_stats[(wave == 4 ? 8 : 0) + i], (unsigned long long)seg_acc[i]);
-    if (wave == 0) atomicAdd(&g_seg_stats[16], 1ull);
+    for (int i = 0; i < 12; ++i) atomicAdd(&g_seg_stats[(wave == 4 ? 12 : 0) + i], (unsigned long long)seg_acc[i]);
+    if (wave == 0) atomicAdd(&g_seg_stats[24], 1ull);
   }
 #endif
 #ifdef PDM_G8S_CLK
@@ -2345,13 +2352,13 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
 
 // the one-problem kernel keeps its own signature (a second by-value GemmArgs in every launch measured +0.7 % on the
 // L/2 forward); the grouped kernel takes both problems
-template <int EPI, int MXO = 0, int SK = 0, int FP8 = 0>
+template <int EPI, int MXO = 0, int SK = 0, int FP8 = 0, int DUAL = 1>
 __global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs p, int tiles_n, int ntiles) {
-  gemm8s_body<EPI, MXO, 0, SK, FP8>(p, tiles_n, ntiles, TV{}, ntiles);
+  gemm8s_body<EPI, MXO, 0, SK, FP8, DUAL>(p, tiles_n, ntiles, TV{}, ntiles);
 }
-template <int EPI>
+template <int EPI, int DUAL = 1>
 __global__ __launch_bounds__(512, 1) void gemm8g_kernel(GemmArgs p, int tiles_n, int ntiles, TV p2, int nt0) {
-  gemm8s_body<EPI, 0, 1>(p, tiles_n, ntiles, p2, nt0);
+  gemm8s_body<EPI, 0, 1, 0, 0, DUAL>(p, tiles_n, ntiles, p2, nt0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2929,10 +2936,10 @@ static long long g_sk_launches = 0;   // stream-K launches so far (host count, t
 void gemm_set_sk(int mode) { g_gemm_sk = mode; }
 int gemm_get_sk() { return g_gemm_sk; }
 long long gemm_sk_launches() { return g_sk_launches; }
-int gemm_seg_stats(unsigned long long* out) {   // reads and clears the -DPDM_G8S_SEG counters (17; synchronises)
+int gemm_seg_stats(unsigned long long* out) {   // reads and clears the -DPDM_G8S_SEG counters (25; synchronises)
   if (hipDeviceSynchronize() != hipSuccess) return 1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg_stats), 17 * sizeof(unsigned long long)) != hipSuccess) return 1;
-  unsigned long long z[17] = {};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg_stats), 25 * sizeof(unsigned long long)) != hipSuccess) return 1;
+  unsigned long long z[25] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_seg_stats), z, sizeof(z)) != hipSuccess;
 }
 int gemm_sk_stats(unsigned long long* out) {   // reads and clears the device counters (synchronises the device)
@@ -3058,6 +3065,11 @@ static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream, const
     (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_RES>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
     (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
     (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_GELU, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 0, 0, 0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_GELU, 0, 0, 0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_RES, 0, 0, 0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 1, 0, 0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_GELU, 1, 0, 0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
       g_num_cus = n;
@@ -3105,9 +3117,13 @@ static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream, const
     }
     return hipGetLastError();
   }
+  // the split-K second A operand (skip_linear's concat) needs the DUAL refill path; every other Linear takes DUAL = 0
+  const bool dual = p.A2 && p.K1 < p.K;
   if (p.out_fp8) {   // fits_8s: bf16 / GELU with the MXFP8 copy as the only output
-    if (epi == EPI_BF16) hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
-    else if (epi == EPI_GELU) hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+    if (epi == EPI_BF16 && dual) hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+    else if (epi == EPI_BF16) hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 1, 0, 0, 0>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+    else if (epi == EPI_GELU && dual) hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 1>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+    else if (epi == EPI_GELU) hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 1, 0, 0, 0>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
@@ -3117,20 +3133,42 @@ static hipError_t launch8s(const GemmArgs& p, int epi, hipStream_t stream, const
       (void)hipFuncSetAttribute((const void*)gemm8g_kernel<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
       (void)hipFuncSetAttribute((const void*)gemm8g_kernel<EPI_GELU>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
       (void)hipFuncSetAttribute((const void*)gemm8g_kernel<EPI_RES>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8g_kernel<EPI_BF16, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8g_kernel<EPI_GELU, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
+      (void)hipFuncSetAttribute((const void*)gemm8g_kernel<EPI_RES, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, S_SMEM);
       attr_g = true;
     }
+    // both problems share A2's presence and K1 (gemm_pair_groups)
     switch (epi) {
-      case EPI_BF16: hipLaunchKernelGGL(gemm8g_kernel<EPI_BF16>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0); break;
-      case EPI_GELU: hipLaunchKernelGGL(gemm8g_kernel<EPI_GELU>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0); break;
-      case EPI_RES: hipLaunchKernelGGL(gemm8g_kernel<EPI_RES>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0); break;
+      case EPI_BF16:
+        if (dual) hipLaunchKernelGGL(gemm8g_kernel<EPI_BF16>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0);
+        else hipLaunchKernelGGL((gemm8g_kernel<EPI_BF16, 0>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0);
+        break;
+      case EPI_GELU:
+        if (dual) hipLaunchKernelGGL(gemm8g_kernel<EPI_GELU>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0);
+        else hipLaunchKernelGGL((gemm8g_kernel<EPI_GELU, 0>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0);
+        break;
+      case EPI_RES:
+        if (dual) hipLaunchKernelGGL(gemm8g_kernel<EPI_RES>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0);
+        else hipLaunchKernelGGL((gemm8g_kernel<EPI_RES, 0>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles, view_of(q), nt0);
+        break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }
   switch (epi) {
-    case EPI_BF16: hipLaunchKernelGGL(gemm8s_kernel<EPI_BF16>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
-    case EPI_GELU: hipLaunchKernelGGL(gemm8s_kernel<EPI_GELU>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
-    case EPI_RES: hipLaunchKernelGGL(gemm8s_kernel<EPI_RES>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles); break;
+    case EPI_BF16:
+      if (dual) hipLaunchKernelGGL(gemm8s_kernel<EPI_BF16>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+      else hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 0, 0, 0, 0>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+      break;
+    case EPI_GELU:
+      if (dual) hipLaunchKernelGGL(gemm8s_kernel<EPI_GELU>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+      else hipLaunchKernelGGL((gemm8s_kernel<EPI_GELU, 0, 0, 0, 0>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+      break;
+    case EPI_RES:
+      if (dual) hipLaunchKernelGGL(gemm8s_kernel<EPI_RES>, dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+      else hipLaunchKernelGGL((gemm8s_kernel<EPI_RES, 0, 0, 0, 0>), dim3(grid), dim3(512), S_SMEM, stream, p, tn, ntiles);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -3151,8 +3189,12 @@ static bool persist_kernels_ok() {
                          (const void*)gemm8s_kernel<EPI_GELU, 0, 1>, (const void*)gemm8s_kernel<EPI_RES, 0, 1>,
                          (const void*)gemm8s_kernel<EPI_BF16, 1, 1>, (const void*)gemm8s_kernel<EPI_GELU, 1, 1>,
                          (const void*)gemm8g_kernel<EPI_BF16>, (const void*)gemm8g_kernel<EPI_GELU>,
-                         (const void*)gemm8g_kernel<EPI_RES>, (const void*)gemm8s_kernel<EPI_BF16, 0, 0, 1>,
-                         (const void*)gemm8s_kernel<EPI_RES, 0, 0, 1>};
+                         (const void*)gemm8g_kernel<EPI_RES>, (const void*)gemm8s_kernel<EPI_BF16, 0, 0, 1, 0>,
+                         (const void*)gemm8s_kernel<EPI_RES, 0, 0, 1, 0>, (const void*)gemm8s_kernel<EPI_BF16, 0, 0, 0, 0>,
+                         (const void*)gemm8s_kernel<EPI_GELU, 0, 0, 0, 0>, (const void*)gemm8s_kernel<EPI_RES, 0, 0, 0, 0>,
+                         (const void*)gemm8s_kernel<EPI_BF16, 1, 0, 0, 0>, (const void*)gemm8s_kernel<EPI_GELU, 1, 0, 0, 0>,
+                         (const void*)gemm8g_kernel<EPI_BF16, 0>, (const void*)gemm8g_kernel<EPI_GELU, 0>,
+                         (const void*)gemm8g_kernel<EPI_RES, 0>};
     ok = 1;
     for (const void* f : fns) {
       hipFuncAttributes at{};
@@ -3209,9 +3251,9 @@ static bool fits_8s_mx(const GemmArgs& p, int epi) {
 static hipError_t launch8s_mx(const GemmArgs& p, int epi, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 0, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_BF16, 0, 0, 1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               S_SMEM_MX);
-    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_RES, 0, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI_RES, 0, 0, 1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               S_SMEM_MX);
     attr_set = true;
   }
@@ -3223,9 +3265,9 @@ static hipError_t launch8s_mx(const GemmArgs& p, int epi, hipStream_t stream) {
   const int ntiles = tm * tn;
   const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
   if (epi == EPI_RES)
-    hipLaunchKernelGGL((gemm8s_kernel<EPI_RES, 0, 0, 1>), dim3(grid), dim3(512), S_SMEM_MX, stream, p, tn, ntiles);
+    hipLaunchKernelGGL((gemm8s_kernel<EPI_RES, 0, 0, 1, 0>), dim3(grid), dim3(512), S_SMEM_MX, stream, p, tn, ntiles);
   else
-    hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 0, 0, 1>), dim3(grid), dim3(512), S_SMEM_MX, stream, p, tn, ntiles);
+    hipLaunchKernelGGL((gemm8s_kernel<EPI_BF16, 0, 0, 1, 0>), dim3(grid), dim3(512), S_SMEM_MX, stream, p, tn, ntiles);
   return hipGetLastError();
 }
 

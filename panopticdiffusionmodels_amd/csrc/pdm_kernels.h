@@ -95,7 +95,7 @@ void gemm_set_sk(int mode);
 int gemm_get_sk();
 long long gemm_sk_launches();
 int gemm_sk_stats(unsigned long long* out3);
-int gemm_seg_stats(unsigned long long* out17);
+int gemm_seg_stats(unsigned long long* out25);
 constexpr int SK_FLAG_WORDS = 256;                       // flags per launch
 constexpr long long SK_SLAB_BYTES = 256LL * 65536 * 4;   // 64 MiB
 
