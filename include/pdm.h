@@ -68,10 +68,10 @@ long long pdm_gemm_sk_launches(void);
  * summed poll time in 10 ns ticks}; reading clears them (synchronises the device) */
 int pdm_gemm_sk_stats(unsigned long long* out3);
 /* diagnostics of -DPDM_G8S_SEG builds (tools/g8s_seg.py): shader cycles per persistent-GEMM main-loop segment summed
- * over workgroups -- wave 0 [0..7] and wave 4 [8..15] (load A, barrier, MFMA A, barrier, load B, barrier, MFMA B,
- * barrier) -- and the workgroup count [16]; reading clears them.  Zeros in production builds (a measurement hook with
- * no reference counterpart) */
-int pdm_gemm_seg_stats(unsigned long long* out17);
+ * over workgroups -- wave 0 [0..11] and wave 4 [12..23] (phase A: fragment reads, refill issue, vmcnt wait, barrier,
+ * MFMAs, barrier; phase B: the same) -- and the workgroup count [24]; reading clears them.  Zeros in production builds
+ * (a measurement hook with no reference counterpart) */
+int pdm_gemm_seg_stats(unsigned long long* out25);
 int pdm_set_attention_algo(int algo);
 
 /* ---- network handle: libs/uvit.py:138-230 UViT, libs/uvit_t2i.py:258-525 UViT (t2i) -------------- */

@@ -1463,12 +1463,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
   constexpr int E = EPI == EPI_RES ? 17 : MXO ? 20 : 16;
   constexpr int ES = FP8 ? 1 : 2;   // operand bytes per element
   constexpr int RW = FP8 ? 9 : 8;   // ring VMEM ops a lane leaves in flight at a phase wait (FP8: + the scale piece)
-#ifndef PDM_G8S_SCHED
-#define PDM_G8S_SCHED 0
-#endif
-  // experimental refill orders (A/B builds, bf16 whole tiles): 2 = a load segment's refills issued before its fragment
-  // reads, 3 = W1 of K-tile g+2 moved from phase B of g to phase A of g+1 (4 + 4 pieces per K-tile instead of 2 + 6)
-  constexpr int XS = (!FP8 && !SK) ? PDM_G8S_SCHED : 0;
+
   typedef int v8i __attribute__((ext_vector_type(8)));
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1867,76 +1862,16 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
 #else
     auto seg = [](int) {};
 #endif
-    for (int kt = kb; kt < ke; ++kt, ++g) {
+    // one K-tile (two phases); ST = the steady state kb < kt < ke - 2 (not a segment's first K-tile, K-tiles g+1 and
+    // g+2 in this segment), where every test below folds at compile time: the loading wave's segment is issue-bound,
+    // so its branches and selects cost time (the first and the last two K-tiles keep the general form)
+    auto ktile = [&](const int kt, auto stc) {
+      constexpr bool ST = decltype(stc)::value;
       const int slot = g & 1;
       const char* buf = smem + slot * BUF;
-      const bool first = kt == kb && after_epi;
-      const bool m1 = kt + 1 < ke || has_next;   // K-tile g+1 exists (this segment's kt+1 or the next one's kbn)
-      const bool m2 = kt + 2 < ke || has_next;   // K-tile g+2 (segments >= 2 K-tiles: the next one's kbn + {0, 1})
-      if constexpr (XS == 2 || XS == 3) {
-        const int k1 = kt + 1 < ke ? kt + 1 : kbn;
-        const int k2 = kt + 2 < ke ? kt + 2 : kbn + (kt + 2 - ke);
-        // XS 3: phase A issues W1(g+1) (moved from phase B of g-1; the prologue / the previous segment's last K-tiles
-        // still issue it there) and A1(g+1)
-        const bool w1 = XS == 3 && m1 && kt + 1 < ke && kt > kb;
-        if constexpr (XS == 2) {
-          if (m1) issue(slot ^ 1, k1, KA1);
-        }
-        read_a(buf, 0);
-        read_w(buf, 0);
-        read_w(buf, 1);
-        lds_done();
-        if constexpr (XS == 3) {
-          if (w1) issue(slot ^ 1, k1, KW1);
-          if (m1) issue(slot ^ 1, k1, KA1);
-        }
-        // retire A1(g); younger: A0 W0 W1 (g+1), A1(g+1) (+ the epilogue's E stores)
-        if (!m1) wait_vmcnt_n<0>();
-        else if (first) wait_vmcnt_n<8 + E>();
-        else wait_vmcnt_n<8>();
-        bar_raw();
-        mma(0, 0);
-        mma(0, 1);
-        bar_raw();
-        if (kt == ke - 2 && has_next) set_tile(nv, m0n, n0n);
-        // XS 3: W1(g+2) stays here when g+2 is the first K-tile of its segment or its segment's second (the next
-        // phase A belongs to the previous tile / the first K-tile's phase A has no W1 to issue)
-        const bool w1b = XS == 2 || !(kt + 2 < ke && kt + 1 > kb);
-        if constexpr (XS == 2) {
-          if (m2) {
-            issue(slot, k2, KA0);
-            issue(slot, k2, KW0);
-            issue(slot, k2, KW1);
-          }
-        }
-        read_a(buf, 1);
-        lds_done();
-        if constexpr (XS == 3) {
-          if (m2) {
-            issue(slot, k2, KA0);
-            issue(slot, k2, KW0);
-            if (w1b) issue(slot, k2, KW1);
-          }
-        }
-        // retire A0 W0 W1(g+1); younger: A1(g+1), A0 W0 (W1) (g+2)
-        if (m2) {
-          const bool w1n = XS == 2 || w1b;   // W1(g+2) issued in this phase
-          if (first) {
-            if (w1n) wait_vmcnt_n<8 + E>();
-            else wait_vmcnt_n<6 + E>();
-          } else {
-            if (w1n) wait_vmcnt_n<8>();
-            else wait_vmcnt_n<6>();
-          }
-        } else if (m1) {
-          wait_vmcnt_n<2>();
-        }
-        bar_raw();
-        mma(1, 0);
-        mma(1, 1);
-        bar_raw();
-        continue;
-      }
+      const bool first = !ST && kt == kb && after_epi;
+      const bool m1 = ST || kt + 1 < ke || has_next;   // K-tile g+1 exists (this segment's kt+1 or the next one's kbn)
+      const bool m2 = ST || kt + 2 < ke || has_next;   // K-tile g+2 (segments >= 2 K-tiles: the next one's kbn + {0, 1})
       // phase A: quadrants (0,0) (0,1); issues A1 of K-tile g+1
       if constexpr (FP8) {
         read_a8(buf, 0);
@@ -1950,7 +1885,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       lds_done();
       seg(0);
       if (m1) {
-        if (!d_nodma) issue(slot ^ 1, kt + 1 < ke ? kt + 1 : kbn, KA1);
+        if (!d_nodma) issue(slot ^ 1, ST || kt + 1 < ke ? kt + 1 : kbn, KA1);
         seg(1);
         if (first && after_slab) wait_vmcnt_n<8 + 32>();
         else if (first) wait_vmcnt_n<RW + E>();
@@ -1976,9 +1911,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       else if (!d_noread) read_a(buf, 1);
       lds_done();
       seg(6);
-      if (kt == ke - 2 && has_next) set_tile(nv, m0n, n0n);
+      if (!ST && kt == ke - 2 && has_next) set_tile(nv, m0n, n0n);
       if (m2) {
-        const int k2 = kt + 2 < ke ? kt + 2 : kbn + (kt + 2 - ke);
+        const int k2 = ST || kt + 2 < ke ? kt + 2 : kbn + (kt + 2 - ke);
         issue_scales(slot, k2);
         if (!d_nodma) {
           issue(slot, k2, KA0);
@@ -2010,6 +1945,18 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       seg(10);
       bar_raw();
       seg(11);
+    };
+    using STF = std::false_type;
+    using STT = std::true_type;
+    if constexpr (SK) {
+      for (int kt = kb; kt < ke; ++kt, ++g) ktile(kt, STF{});
+    } else {
+      int kt = kb;
+      ktile(kt, STF{});   // nk >= 4 (fits_8s / fits_8s_mx): the first K-tile, then the steady ones
+      ++kt;
+      ++g;
+      for (; kt + 2 < ke; ++kt, ++g) ktile(kt, STT{});
+      for (; kt < ke; ++kt, ++g) ktile(kt, STF{});
     }
     if (wave < 4) bar_raw();   // rejoin the stagger
 
