@@ -1882,15 +1882,19 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
         read_w(buf, 0);
         read_w(buf, 1);
       }
-      lds_done();
+      // a phase's refills issue behind its fragment reads and before their lgkmcnt wait: they write ring halves no
+      // wave reads in this phase, and their issue (the TA takes one 1 KiB piece at a time) overlaps the reads'
+      // latency (L/2 bench 63.7 -> 64.5 img/s same box, profiles/r06q; issued before the reads: 63.6)
       seg(0);
       if (m1) {
         if (!d_nodma) issue(slot ^ 1, ST || kt + 1 < ke ? kt + 1 : kbn, KA1);
+        lds_done();
         seg(1);
         if (first && after_slab) wait_vmcnt_n<8 + 32>();
         else if (first) wait_vmcnt_n<RW + E>();
         else wait_vmcnt_n<RW>();
       } else {
+        lds_done();
         wait_vmcnt_n<0>();
       }
       seg(2);
@@ -1907,25 +1911,26 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       bar_raw();
       seg(5);
       // phase B: quadrants (1,0) (1,1); issues A0 W0 W1 of K-tile g+2 (the next segment's from kt = ke-2 on)
+      if (!ST && kt == ke - 2 && has_next) set_tile(nv, m0n, n0n);
+      const int k2 = ST || kt + 2 < ke ? kt + 2 : kbn + (kt + 2 - ke);
       if constexpr (FP8) read_a8(buf, 1);
       else if (!d_noread) read_a(buf, 1);
-      lds_done();
       seg(6);
-      if (!ST && kt == ke - 2 && has_next) set_tile(nv, m0n, n0n);
       if (m2) {
-        const int k2 = ST || kt + 2 < ke ? kt + 2 : kbn + (kt + 2 - ke);
         issue_scales(slot, k2);
         if (!d_nodma) {
           issue(slot, k2, KA0);
           issue(slot, k2, KW0);
           issue(slot, k2, KW1);
         }
+        lds_done();
         seg(7);
         if (first && after_slab) wait_vmcnt_n<8 + 32>();
         else if (first) wait_vmcnt_n<RW + E>();
         else wait_vmcnt_n<RW>();
-      } else if (m1) {
-        wait_vmcnt_n<2>();
+      } else {
+        lds_done();
+        if (m1) wait_vmcnt_n<2>();
       }
       seg(8);
       bar_raw();
