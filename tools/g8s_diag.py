@@ -42,7 +42,7 @@ for _ in range(300):
     _lib.gemm_ex(_lib.EPI_BF16, A[:, :D], _w, None, out=outb[:, :3 * D])
 torch.cuda.synchronize()
 
-VARIANTS = [("fwd", 0), ("noepi", 16)]
+VARIANTS = [("fwd", 0), ("noepi", 16), ("nostore", 32)]
 for name, N, K, kind in [("qkv", 3 * D, D, "ln"), ("proj", D, D, "res"), ("fc1", 4 * D, D, "ln_gelu"),
                          ("fc2", D, 4 * D, "res"), ("skip", D, 2 * D, "res")]:
     W = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).bfloat16()
