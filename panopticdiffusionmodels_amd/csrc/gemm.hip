@@ -2102,18 +2102,31 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
 #pragma unroll
           for (int qj = 0; qj < 2; ++qj) {
             unsigned u[2][2];
+            f32x4 v[2];
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni) {
-              f32x4 v = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
+              v[ni] = acc[((qi * 2 + qj) * 2 + ni) * 4 + mi];
               // rstd * (acc - mean * colsum) + bias as acc * rstd + (bias - mean * rstd * colsum): 2 FMAs per value
-              if (ln) v = v * mr.y + (bv[qj][ni] - (mr.x * mr.y) * cs[qj][ni]);
-              else v += bv[qj][ni];
-              if constexpr (EPI == EPI_GELU) {   // exact-erf GELU only (quick GELU: gemm8d, fits_8s)
-                const f32x2 lo = gelu_erf2(f32x2{v[0], v[1]}), hi = gelu_erf2(f32x2{v[2], v[3]});
-                v = f32x4{lo[0], lo[1], hi[0], hi[1]};
+              if (ln) v[ni] = v[ni] * mr.y + (bv[qj][ni] - (mr.x * mr.y) * cs[qj][ni]);
+              else v[ni] += bv[qj][ni];
+            }
+            if constexpr (EPI == EPI_GELU && MXO && SK) {   // (the stream-K MXFP8-output form spills with 4 pairs)
+#pragma unroll
+              for (int ni = 0; ni < 2; ++ni) {
+                const f32x2 lo = gelu_erf2(f32x2{v[ni][0], v[ni][1]}), hi = gelu_erf2(f32x2{v[ni][2], v[ni][3]});
+                v[ni] = f32x4{lo[0], lo[1], hi[0], hi[1]};
               }
-              u[ni][0] = pack_bf16x2(v[0], v[1]);
-              u[ni][1] = pack_bf16x2(v[2], v[3]);
+            } else if constexpr (EPI == EPI_GELU) {   // exact-erf GELU only (quick GELU: gemm8d, fits_8s); 4 pairs interleaved
+              f32x2 x2[4] = {f32x2{v[0][0], v[0][1]}, f32x2{v[0][2], v[0][3]}, f32x2{v[1][0], v[1][1]},
+                             f32x2{v[1][2], v[1][3]}};
+              gelu_erf2x4(x2);
+              v[0] = f32x4{x2[0][0], x2[0][1], x2[1][0], x2[1][1]};
+              v[1] = f32x4{x2[2][0], x2[2][1], x2[3][0], x2[3][1]};
+            }
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+              u[ni][0] = pack_bf16x2(v[ni][0], v[ni][1]);
+              u[ni][1] = pack_bf16x2(v[ni][2], v[ni][3]);
             }
             if constexpr (MXO) {
               // MXFP8 of the bf16-rounded values (as gemm8d's staged epilogue): the 32-column block qj*128 + wn*32

@@ -59,6 +59,29 @@ __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
   for (int k = 8; k >= 0; --k) p = __builtin_elementwise_fma(p, v, f32x2(c[k]));
   return x * __builtin_elementwise_fma(s, p, f32x2(0.5f));
 }
+// gelu_erf2 on four independent pairs with each Horner step issued for all four before the next: hipcc otherwise
+// emits one pair's 13 dependent packed ops back to back (an s_nop between each), so a GELU epilogue runs at the
+// VALU latency, not its issue rate.  Bit-identical to gelu_erf (the same operations per element).
+__device__ __forceinline__ void gelu_erf2x4(f32x2 (&x)[4]) {
+  constexpr float c[10] = {PDM_GELU_COEFFS};
+  f32x2 s[4], v[4], p[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s[j] = x[j] * (1.0f / 4.5f);
+    s[j][0] = __builtin_amdgcn_fmed3f(s[j][0], -1.0f, 1.0f);
+    s[j][1] = __builtin_amdgcn_fmed3f(s[j][1], -1.0f, 1.0f);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = __builtin_elementwise_fma(s[j], s[j], f32x2(-0.5f));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) p[j] = __builtin_elementwise_fma(f32x2(c[9]), v[j], f32x2(c[8]));
+#pragma unroll
+  for (int k = 7; k >= 0; --k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = __builtin_elementwise_fma(p[j], v[j], f32x2(c[k]));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) x[j] = x[j] * __builtin_elementwise_fma(s[j], p[j], f32x2(0.5f));
+}
 #undef PDM_GELU_COEFFS
 
 // quick GELU (transformers QuickGELUActivation, CLIP text encoder): x * sigmoid(1.702 x)
