@@ -894,6 +894,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
 // HN (half-N, N <= 128, SCHED 2 only): a 256 x 128 tile -- the W1 half is never loaded and only the qj = 0
 // quadrants are computed (the decoder's 128-channel 512^2 convs would otherwise waste half of every 256 x 256
 // tile or run on the 128-tile kernel); the epilogue is the 256-wide one, columns >= N are never stored.
+// implicit-GEMM conv: byte offset of tap (dy, dx) of the output pixel packed in pix (b << 18 | y << 9 | x, -1 past
+// M) in the NHWC source (nearest-upsampled by conv_up), OOB in the zero padding.  No division: 24-bit multiplies only
+// (fits_rsrc: H, W <= 512, b < 8192, and every byte offset < 2^31, so the pixel index stays below 2^24).
+__device__ __forceinline__ unsigned conv_off(const GemmArgs& p, int pix, int dy, int dx, unsigned sb) {
+  // the decode of pix stays in the loop: hoisted per piece (y, x, b * H) it cost 16 more VGPRs and the 512-row tile
+  // kernel spilled inside its K-loop (a scratch reload + vmcnt(0) drain per K-tile)
+  asm volatile("" : "+v"(pix));
+  const int yy = ((pix >> 9) & 511) + dy, xx = (pix & 511) + dx;
+  if (pix < 0 || (unsigned)yy >= (unsigned)p.convH || (unsigned)xx >= (unsigned)p.convW) return OOB;
+  const int sh = p.conv_up;
+  const unsigned row = __umul24((unsigned)(pix >> 18), (unsigned)(p.convH >> sh)) + (unsigned)(yy >> sh);
+  const unsigned px = __umul24(row, (unsigned)(p.convW >> sh)) + (unsigned)(xx >> sh);
+  return __umul24(px, (unsigned)(p.convC * 2)) + sb;
+}
+
 template <int EPI, int CONV, int SCHED, int HN = 0>
 __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n, int nwg) {
   static_assert(!HN || SCHED == 2, "the half-N tile exists in the SCHED 2 schedule only");
@@ -945,7 +960,7 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
   // per-lane offsets of this wave's two 1 KiB pieces (8 rows x 128 B) in each half (h) of A and W
   const int prow = lane >> 3, pch = lane & 7;
   unsigned a1off[2][2], a2off[2][2], woff[2][2];
-  int cpix[2][2];   // conv: (b * H + y) << 12 | x of the piece row's output pixel, -1 past M
+  int cpix[2][2];   // conv: b << 18 | y << 9 | x of the piece row's output pixel, -1 past M (fits_rsrc: H, W <= 512)
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = (wave * 2 + i) * 8 + prow;
@@ -956,7 +971,7 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
       if constexpr (CONV) {
         if (gm < p.M) {
           const int hw = p.convH * p.convW, b = gm / hw, r = gm - b * hw, y = r / p.convW;
-          cpix[h][i] = ((b * p.convH + y) << 12) | (r - y * p.convW);
+          cpix[h][i] = (b << 18) | (y << 9) | (r - y * p.convW);
         } else {
           cpix[h][i] = -1;
         }
@@ -984,15 +999,7 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
       } else if constexpr (CONV) {
         const int tap = k0 / p.convC, ci0 = k0 - tap * p.convC;
         const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-        const int pix = cpix[kind][i];
-        const int yy = ((pix >> 12) % p.convH) + dy, xx = (pix & 4095) + dx;
-        const int bb = (pix >> 12) / p.convH;
-        unsigned off = OOB;
-        if (pix >= 0 && yy >= 0 && yy < p.convH && xx >= 0 && xx < p.convW) {
-          const int sh = p.conv_up, Hs = p.convH >> sh, Ws = p.convW >> sh;
-          off = (unsigned)(((bb * Hs + (yy >> sh)) * Ws + (xx >> sh)) * p.convC) * 2u + a1off[kind][i];
-        }
-        dma16(ra1, off, ci0 * 2, d);
+        dma16(ra1, conv_off(p, cpix[kind][i], dy, dx, a1off[kind][i]), ci0 * 2, d);
       } else {
         if (k0 < p.K1) dma16(ra1, a1off[kind][i], k0 * 2, d);
         else dma16(ra2, a2off[kind][i], (k0 - p.K1) * 2, d);
@@ -1101,20 +1108,20 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
       const bool m1 = kt + 1 < nk, m2 = kt + 2 < nk;
       read_a(buf, 0);
       read_w(buf, 0);
-      lds_done();
-      if (m1) { issue(kt + 1, KA1); asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }   // A1(kt)
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (m1) { issue(kt + 1, KA1); lds_done(); asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }   // A1(kt)
+      else { lds_done(); asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
       bar_raw();
       mma(0, 0);
       bar_raw();
       read_a(buf, 1);
-      lds_done();
       if (m2) {
         issue(kt + 2, KA0);
         issue(kt + 2, KW0);
+        lds_done();
         asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // A0 W0 (kt+1)
-      } else if (m1) {
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      } else {
+        lds_done();
+        if (m1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       }
       bar_raw();
       mma(1, 0);
@@ -1146,23 +1153,23 @@ __global__ __launch_bounds__(512, 1) void gemm8d_kernel(GemmArgs p, int tiles_n,
       read_a(buf, 0);
       read_w(buf, 0);
       read_w(buf, 1);
-      lds_done();
-      if (m1) { issue(kt + 1, KA1); asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }   // A1(kt)
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (m1) { issue(kt + 1, KA1); lds_done(); asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }   // A1(kt)
+      else { lds_done(); asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
       bar_raw();
       mma(0, 0);
       mma(0, 1);
       bar_raw();
       // phase B
       read_a(buf, 1);
-      lds_done();
       if (m2) {
         issue(kt + 2, KA0);
         issue(kt + 2, KW0);
         issue(kt + 2, KW1);
+        lds_done();
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // A0 W0 W1 (kt+1)
-      } else if (m1) {
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      } else {
+        lds_done();
+        if (m1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       }
       bar_raw();
       mma(1, 0);
@@ -2377,7 +2384,7 @@ __global__ __launch_bounds__(512, 1) void gemm8t_kernel(GemmArgs p, int nwg) {
       if constexpr (CONV) {
         if (gm < p.M) {
           const int hw = p.convH * p.convW, b = gm / hw, r = gm - b * hw, y = r / p.convW;
-          cpix[h][i] = ((b * p.convH + y) << 12) | (r - y * p.convW);
+          cpix[h][i] = (b << 18) | (y << 9) | (r - y * p.convW);
         } else {
           cpix[h][i] = -1;
         }
@@ -2403,15 +2410,7 @@ __global__ __launch_bounds__(512, 1) void gemm8t_kernel(GemmArgs p, int nwg) {
       } else if constexpr (CONV) {
         const int tap = k0 / p.convC, ci0 = k0 - tap * p.convC;
         const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-        const int pix = cpix[kind][i];
-        const int yy = ((pix >> 12) % p.convH) + dy, xx = (pix & 4095) + dx;
-        const int bb = (pix >> 12) / p.convH;
-        unsigned off = OOB;
-        if (pix >= 0 && yy >= 0 && yy < p.convH && xx >= 0 && xx < p.convW) {
-          const int sh = p.conv_up, Hs = p.convH >> sh, Ws = p.convW >> sh;
-          off = (unsigned)(((bb * Hs + (yy >> sh)) * Ws + (xx >> sh)) * p.convC) * 2u + sbv[i];
-        }
-        dma16(ra1, off, ci0 * 2, d);
+        dma16(ra1, conv_off(p, cpix[kind][i], dy, dx, sbv[i]), ci0 * 2, d);
       } else {
         if (k0 < p.K1) dma16(ra1, a1off[kind][i], k0 * 2, d);
         else dma16(ra2, a2off[kind][i], (k0 - p.K1) * 2, d);
@@ -2485,12 +2484,13 @@ __global__ __launch_bounds__(512, 1) void gemm8t_kernel(GemmArgs p, int nwg) {
     read_a(buf, 0);
     read_w(buf);
     read_a(buf, 1);
-    lds_done();
     if (m1) {
       issue(kt + 1, 2);
       issue(kt + 1, 3);
+      lds_done();
       asm volatile("s_waitcnt vmcnt(10)" ::: "memory");   // A2 A3 (kt)
     } else {
+      lds_done();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     bar_raw();
@@ -2500,14 +2500,15 @@ __global__ __launch_bounds__(512, 1) void gemm8t_kernel(GemmArgs p, int nwg) {
     // phase B
     read_a(buf, 2);
     read_a(buf, 3);
-    lds_done();
     if (m2) {
       issue(kt + 2, 0);
       issue(kt + 2, KW);
       issue(kt + 2, 1);
+      lds_done();
       asm volatile("s_waitcnt vmcnt(10)" ::: "memory");   // A0 W A1 (kt+1)
-    } else if (m1) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      lds_done();
+      if (m1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     }
     bar_raw();
     mma(2);
@@ -2758,24 +2759,24 @@ __global__ __launch_bounds__(512, 1) void gemm_mx_kernel(GemmArgs p, int tiles_n
     read_a(buf, 0);
     read_w(buf);
     read_scales(kt);
-    lds_done();
-    if (m1) { issue(kt + 1, KA1); asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); }   // A1(kt)
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (m1) { issue(kt + 1, KA1); lds_done(); asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); }   // A1(kt)
+    else { lds_done(); asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
     bar_raw();
     mma(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
     mma(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
     bar_raw();
     // phase B
     read_a(buf, 1);
-    lds_done();
     if (m2) {
       issue_scales(kt + 2);
       issue(kt + 2, KA0);
       issue(kt + 2, KW0);
       issue(kt + 2, KW1);
+      lds_done();
       asm volatile("s_waitcnt vmcnt(9)" ::: "memory");   // S A0 W0 W1 (kt+1)
-    } else if (m1) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      lds_done();
+      if (m1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     }
     bar_raw();
     mma(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
@@ -3268,7 +3269,8 @@ static bool fits_rsrc(const GemmArgs& p) {
   else a1 = (long long)p.M * p.lda1 * es;
   const long long a2 = p.A2 ? (long long)p.M * p.lda2 * 2 : 0;
   const long long w = (long long)p.N * (p.ldw > 0 ? p.ldw : p.K) * es;
-  return a1 < lim && a2 < lim && w < lim && (!p.conv || p.convW < 4096);
+  return a1 < lim && a2 < lim && w < lim &&
+         (!p.conv || (p.convW <= 512 && p.convH <= 512 && p.M / (p.convH * p.convW) < 8192));   // conv_off's packing
 }
 
 // the second residual output of a launch whose kernel has no out2 store (the 128 tile, a split launch): the rows
