@@ -3332,12 +3332,11 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
                          (p.out_bf16 && (p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15))))) algo = 1;
   if (p.fp8) {
     if (!fits_rsrc(p)) return hipErrorInvalidValue;
-    // the persistent form on request only (algo 11): measured 3.5-4.7 % slower than gemm_mx_kernel on the H/4 qkv
-    // at 50-190 rows (tools/mx_qkv_bench.py), so the automatic choice stays one tile per workgroup
-    // the persistent residual form from 64 sequences of 258 tokens up: H/4 proj at 100 rows 64.3 -> 60.6 us, at the
-    // bench's 50-row lanes 36.4 vs 36.8 us (tools/mx_res_bench.py, profiles/r06j); outputs bit-identical
-    if ((g_gemm_algo == 11 || (g_gemm_algo == 0 && epi == EPI_RES && g_mx_res_persist && p.M >= 16384)) &&
-        fits_8s_mx(p, epi))
+    // the persistent form under the automatic policy from 16 sequences of 258 tokens up (round 6, after its
+    // issue-path changes): the H/4 forward at the bench's 50-row lanes 13.12 -> 12.99 ms with it on every MXFP8
+    // shape (qkv with the centred LayerNorm consumer, proj, fc2; tools/forward_algo_ab.py, profiles/r06al); the
+    // residual form alone: 64.3 -> 57.2 us at 100 rows, parity at 25-50 (tools/mx_res_bench.py, profiles/r06v)
+    if ((g_gemm_algo == 11 || (g_gemm_algo == 0 && g_mx_res_persist && p.M >= 4096)) && fits_8s_mx(p, epi))
       return launch8s_mx(p, epi, stream);
     return launch_mx(p, epi, stream);
   }
