@@ -294,6 +294,9 @@ int pdm_decoder_set_param(pdm_decoder* d, const char* name, const void* dev_ptr,
 int pdm_decoder_workspace_size(const pdm_decoder* d, int batch, size_t* bytes);
 int pdm_decoder_decode(pdm_decoder* d, const float* z, float* img, int batch, void* workspace,
                        size_t workspace_bytes, void* stream);
+/* GroupNorm statistics from the producing convolution / linear epilogues (default 1); 0 = a separate statistics
+ * pass over every GroupNorm input (A/B and parity tests).  Process-wide; not thread-safe against a running decode. */
+int pdm_decoder_set_gn_fusion(int on);
 
 /* ---- output stage (utils.sample2dir, utils.py:561-640) ------------------------------------------
  * Decoded images fp32 [B, C, H, W] -> uint8 [B, H, W, C]: unpreprocess (datasets.py:104-108) followed by

@@ -160,6 +160,7 @@ _SIGS = {
     "pdm_decoder_workspace_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "pdm_decoder_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "pdm_decoder_set_gn_fusion": (ctypes.c_int, [ctypes.c_int]),
     # training step (include/pdm.h "training")
     "pdm_train_create": (ctypes.c_int, [ctypes.POINTER(PdmUvitCfg), ctypes.POINTER(ctypes.c_void_p)]),
     "pdm_train_destroy": (ctypes.c_int, [ctypes.c_void_p]),

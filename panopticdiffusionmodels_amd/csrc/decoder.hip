@@ -460,13 +460,20 @@ struct DCtx {
   const pdm_decoder* d;
   hipStream_t s;
   const DWork* w;
+  // set by the GEMM / conv that just wrote the next GroupNorm's input with GemmArgs::gn_part (its partials in w->part,
+  // 256-pixel chunks), cleared by the GroupNorm that consumes them
+  bool* gn_ready;
 };
 
 template <typename T>
 int groupnorm(const DCtx& c, const T* x, int B, int P, int C, const std::string& norm, bf16* y, bool swish) {
-  const int pix = pdm::gn_pix(C);
+  // statistics pass: skipped when the producing epilogue already left the partials (one read of x fewer)
+  const bool pre = *c.gn_ready;
+  *c.gn_ready = false;
+  const int pix = pre ? 256 : pdm::gn_pix(C);
   const int nchunk = (P + pix - 1) / pix;
-  hipLaunchKernelGGL(pdm::gn_partial_kernel<T>, dim3(nchunk, B), dim3(256), 0, c.s, x, P, C, nchunk, pix, c.w->part);
+  if (!pre)
+    hipLaunchKernelGGL(pdm::gn_partial_kernel<T>, dim3(nchunk, B), dim3(256), 0, c.s, x, P, C, nchunk, pix, c.w->part);
   hipLaunchKernelGGL(pdm::gn_final_kernel, dim3((B * 32 + 3) / 4), dim3(256), 0, c.s, c.w->part, nchunk,
                      (double)P * (C / 32), 1e-6f, c.w->stats, B);
   if (C % 8 || C > 2048) return dfail(PDM_ERR_ARG, "decoder: GroupNorm needs C % 8 == 0 and C <= 2048");
@@ -481,27 +488,38 @@ int groupnorm(const DCtx& c, const T* x, int B, int P, int C, const std::string&
 }
 
 // implicit-GEMM conv3x3 (in: bf16 NHWC [B, res>>up, res>>up, cin]) -> epilogue
+bool g_gn_fusion = true;   // pdm_decoder_set_gn_fusion
+
+// gn_P > 0: the output is the next GroupNorm's input (gn_P pixels per image): its epilogue also writes the GroupNorm
+// partials where it can (pdm::gemm_gn_fusable; c.gn_ready tells the GroupNorm)
+int launch_gn(const DCtx& c, pdm::GemmArgs& a, int epi, int gn_P) {
+  if (gn_P > 0 && g_gn_fusion) {
+    a.gn_part = c.w->part; a.gn_P = gn_P; a.gn_cpg = a.N / 32;
+    if (!pdm::gemm_gn_fusable(a, epi)) a.gn_part = nullptr;
+  }
+  D_CHECK(pdm::gemm_check(a, epi));
+  D_HIP(pdm::gemm_launch(a, epi, c.s));
+  *c.gn_ready = a.gn_part != nullptr;
+  return PDM_OK;
+}
+
 int conv3(const DCtx& c, const bf16* in, int B, int res, int cin, int cout, const std::string& name, int epi,
-          bf16* ob, float* of, int accumulate, int up = 0) {
+          bf16* ob, float* of, int accumulate, int up = 0, bool gn = false) {
   pdm::GemmArgs a{};
   a.A1 = in; a.lda1 = cin; a.K1 = 9 * cin;
   a.W = c.d->w(name + ".weight"); a.bias = c.d->f(name + ".bias");
   a.M = B * res * res; a.N = cout; a.K = 9 * cin;
   a.out_bf16 = ob; a.ldo = cout; a.out_f32 = of; a.ldr = cout; a.accumulate = accumulate;
   a.conv = 1; a.convH = res; a.convW = res; a.convC = cin; a.conv_up = up; a.zero = c.w->zero;
-  D_CHECK(pdm::gemm_check(a, epi));
-  D_HIP(pdm::gemm_launch(a, epi, c.s));
-  return PDM_OK;
+  return launch_gn(c, a, epi, gn ? res * res : 0);
 }
 
 int linear(const DCtx& c, const bf16* A, int M, int K, const bf16* W, const float* bias, int N, int epi, bf16* ob,
-           float* of, int accumulate) {
+           float* of, int accumulate, int gn_P = 0) {
   pdm::GemmArgs a{};
   a.A1 = A; a.lda1 = K; a.K1 = K; a.W = W; a.bias = bias; a.M = M; a.N = N; a.K = K;
   a.out_bf16 = ob; a.ldo = N; a.out_f32 = of; a.ldr = N; a.accumulate = accumulate;
-  D_CHECK(pdm::gemm_check(a, epi));
-  D_HIP(pdm::gemm_launch(a, epi, c.s));
-  return PDM_OK;
+  return launch_gn(c, a, epi, gn_P);
 }
 
 // ResnetBlock (libs/autoencoder.py:75-134): X (fp32 NHWC, cin) -> X (cout) in place (or via X2 for nin).
@@ -512,7 +530,7 @@ int resblock(const DCtx& c, float*& X, float*& X2, int B, int res, int cin, int 
   const DWork& w = *c.w;
   const int P = res * res;
   D_TRY(groupnorm<float>(c, X, B, P, cin, p + ".norm1", w.G, true));
-  D_TRY(conv3(c, w.G, B, res, cin, cout, p + ".conv1", pdm::EPI_BF16, w.H, nullptr, 0));
+  D_TRY(conv3(c, w.G, B, res, cin, cout, p + ".conv1", pdm::EPI_BF16, w.H, nullptr, 0, 0, true));
   D_TRY(groupnorm<bf16>(c, w.H, B, P, cout, p + ".norm2", w.G, true));
   if (cin != cout) {
     // x = nin_shortcut(x): 1x1 conv = GEMM on a bf16 copy of x, into X2; then X2 += conv2(h)
@@ -522,12 +540,12 @@ int resblock(const DCtx& c, float*& X, float*& X2, int B, int res, int cin, int 
     }
     D_TRY(linear(c, xb, B * P, cin, c.d->w(p + ".nin_shortcut.weight"), c.d->f(p + ".nin_shortcut.bias"), cout,
                  pdm::EPI_F32, nullptr, X2, 0));
-    D_TRY(conv3(c, w.G, B, res, cout, cout, p + ".conv2", pdm::EPI_F32, copy_out, X2, 1));
+    D_TRY(conv3(c, w.G, B, res, cout, cout, p + ".conv2", pdm::EPI_F32, copy_out, X2, 1, 0, true));
     float* t = X;
     X = X2;
     X2 = t;
   } else {
-    D_TRY(conv3(c, w.G, B, res, cout, cout, p + ".conv2", pdm::EPI_F32, copy_out, X, 1));
+    D_TRY(conv3(c, w.G, B, res, cout, cout, p + ".conv2", pdm::EPI_F32, copy_out, X, 1, 0, true));
   }
   return PDM_OK;
 }
@@ -564,7 +582,7 @@ int attnblock(const DCtx& c, float* X, int B, int res, int C, const std::string&
   }
   // x + proj_out(o)
   D_TRY(linear(c, w.O, B * hw, C, c.d->w(p + ".proj_out.weight"), c.d->f(p + ".proj_out.bias"), C, pdm::EPI_F32,
-               nullptr, X, 1));
+               nullptr, X, 1, hw));
   return PDM_OK;
 }
 
@@ -621,6 +639,11 @@ int pdm_decoder_create(const pdm_decoder_cfg* cfg, pdm_decoder** out) {
   return PDM_OK;
 }
 
+int pdm_decoder_set_gn_fusion(int on) {
+  g_gn_fusion = on != 0;
+  return PDM_OK;
+}
+
 int pdm_decoder_destroy(pdm_decoder* d) {
   delete d;
   return PDM_OK;
@@ -661,7 +684,8 @@ int pdm_decoder_decode(pdm_decoder* d, const float* z, float* img, int B, void* 
   DWork w = dlayout(d, B, (char*)workspace);
   if (w.bytes > workspace_bytes) return dfail(PDM_ERR_ARG, "pdm_decoder_decode: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  DCtx c{d, s, &w};
+  bool gn_ready = false;
+  DCtx c{d, s, &w, &gn_ready};
   D_HIP(hipMemsetAsync(w.zero, 0, 256, s));
   const int T = d->top_ch;
   int res = d->h0;
@@ -692,7 +716,7 @@ int pdm_decoder_decode(pdm_decoder* d, const float* z, float* img, int B, void* 
       const int next = d->cfg.ch * d->cfg.ch_mult[lvl - 1];
       bf16* cp = next != cin ? w.XB : nullptr;   // the next level's first block changes width: its nin input
       D_TRY(conv3(c, w.H, B, res, cin, cin, "decoder.up." + std::to_string(lvl) + ".upsample.conv", pdm::EPI_F32,
-                  cp, X2, 0, 1));
+                  cp, X2, 0, 1, true));
       xb = cp;
       float* t = X;
       X = X2;

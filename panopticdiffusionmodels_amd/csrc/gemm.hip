@@ -270,6 +270,43 @@ __device__ __forceinline__ float sum32(float x) {
   return x + __shfl_xor(x, 16, 64);
 }
 
+// GroupNorm partials in the 256-tile epilogue (GemmArgs::gn_part): a thread stores 8 consecutive columns
+// n0 + (tid & 31) * 8 of 16 rows of the tile; gn_cpg >= 8 puts them in one group (slot 0), gn_cpg = 4 in two.
+__device__ __forceinline__ void gn_acc(const GemmArgs& p, const float (&f)[8], float (&gs)[2], float (&gq)[2]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int sl = p.gn_cpg == 4 ? (j >> 2) : 0;
+    gs[sl] += f[j];
+    gq[sl] = fmaf(f[j], f[j], gq[sl]);
+  }
+}
+// the 16 row-threads of each column octet and the octets of a group combine through LDS in fp64 (as
+// gn_partial_kernel's per-group pass); one thread per group of the tile writes its 256-row chunk's partial.
+// Callers: after a barrier behind the tile's last LDS read; the caller's next LDS write follows a barrier.
+__device__ __forceinline__ void gn_store(const GemmArgs& p, char* smem, int tid, int m0, int n0, const float (&gs)[2],
+                                         const float (&gq)[2]) {
+  float2* red = reinterpret_cast<float2*>(smem);   // [16 row-threads][32 octets][2 slots]
+  red[((tid >> 5) * 32 + (tid & 31)) * 2] = make_float2(gs[0], gq[0]);
+  red[((tid >> 5) * 32 + (tid & 31)) * 2 + 1] = make_float2(gs[1], gq[1]);
+  __syncthreads();
+  const int cpg = p.gn_cpg, ngr = min(256, p.N - n0) / cpg;
+  if (tid < ngr) {
+    double s = 0.0, q = 0.0;
+    const int c0 = tid * cpg / 8, nc = cpg >= 8 ? cpg / 8 : 1, sl = cpg >= 8 ? 0 : (tid & 1);
+    for (int c = c0; c < c0 + nc; ++c)
+      for (int r = 0; r < 16; ++r) {
+        const float2 v = red[(r * 32 + c) * 2 + sl];
+        s += v.x;
+        q += v.y;
+      }
+    const int b = m0 / p.gn_P, chunk = (m0 - b * p.gn_P) >> 8, g = n0 / cpg + tid;
+    double* o = p.gn_part + (((size_t)b * (p.gn_P >> 8) + chunk) * 32 + g) * 2;
+    o[0] = s;
+    o[1] = q;
+  }
+  __syncthreads();
+}
+
 // Epilogue of a 256x256 tile (needs 128 KiB of LDS; the staging ring is free by then).
 //  EPI_RES: the fp32 path below with a bf16 residual stream (res_in read, bf16 out_bf16 written, 16-byte rows).
 //  bf16 / GELU: the bf16 tile is written to LDS with a row-XOR chunk swizzle, then stored row-contiguously
@@ -374,6 +411,19 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
         if (m < p.M && n < p.N) mx_store8(p.out_fp8, p.ldo8, p.out_scale, p.out_scale_ld, m, n, q, e8, (tid & 3) == 0);
       }
     }
+    if (p.gn_part) {   // GroupNorm partials of the rounded values (exactly what the GroupNorm reads)
+      float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const bf16x8 b8 = __builtin_bit_cast(bf16x8, v[it]);
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (float)b8[j];
+        gn_acc(p, f, gs, gq);
+      }
+      __syncthreads();   // every thread's LDS read-back is done: the reduction reuses the staging area
+      gn_store(p, smem, tid, m0, n0, gs, gq);
+    }
     if (!p.out_bf16) return;
     if ((p.dbg_tile0 & 4) && ((n0 >> 8) & 1)) return;   // timing experiment: odd column tiles store nothing
     if (full) {
@@ -439,6 +489,7 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
     b0 = *reinterpret_cast<const f32x4*>(p.bias + n);
     if (n + 4 < p.N) b1 = *reinterpret_cast<const f32x4*>(p.bias + n + 4);
   }
+  float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};   // GroupNorm partials (p.gn_part) of the thread's stored rows
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
@@ -523,6 +574,10 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
           f32x4* r = reinterpret_cast<f32x4*>(p.out_f32 + m * p.ldr + n);
           r[0] = v0[i];
           r[1] = v1[i];
+          if (p.gn_part) {
+            const float f[8] = {v0[i][0], v0[i][1], v0[i][2], v0[i][3], v1[i][0], v1[i][1], v1[i][2], v1[i][3]};
+            gn_acc(p, f, gs, gq);
+          }
           if (p.out_bf16) {
             bf16x8 o;
 #pragma unroll
@@ -560,6 +615,10 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
             }
             r[0] = a;
             r[1] = b;
+            if (p.gn_part) {   // (gn_part tiles are whole: gemm_gn_fusable)
+              const float f[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+              gn_acc(p, f, gs, gq);
+            }
             if (p.out_bf16) {
               bf16x8 o;
 #pragma unroll
@@ -575,6 +634,9 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& p, const f32x4 (&acc
       }
     }
     __syncthreads();
+  }
+  if constexpr (EPI == EPI_F32) {
+    if (p.gn_part) gn_store(p, smem, tid, m0, n0, gs, gq);
   }
 }
 
@@ -3304,7 +3366,24 @@ hipError_t gemm_launch_pair(const GemmArgs& a, const GemmArgs& b, int epi, hipSt
   return e != hipSuccess ? e : gemm_launch(b1, epi, stream);
 }
 
+// GemmArgs::gn_part: only the gemm8d (algo 7) and gemm8t (algo 9) epilogues write GroupNorm partials, on whole
+// 256-row tiles of whole images; mirrors gemm_launch's automatic choice for conv / fp32 launches
+bool gemm_gn_fusable(const GemmArgs& p, int epi) {
+  if (g_gemm_algo != 0 || (epi != EPI_F32 && epi != EPI_BF16) || !(p.conv || epi == EPI_F32)) return false;
+  if (p.fp8 || p.out_fp8 || p.batch > 1 || p.a_rows_per_group > 0 || p.ln_stats || p.stats_out || p.A2) return false;
+  if (p.gn_P <= 0 || p.gn_P % 256 || p.M % p.gn_P || p.N % 32 || p.gn_cpg * 32 != p.N) return false;
+  if (p.gn_cpg != 4 && p.gn_cpg != 8 && p.gn_cpg != 16 && p.gn_cpg != 32) return false;
+  const bool a7 = p.M >= 4096 && p.N >= 256, a9 = p.M >= 65536 && p.N > 96 && p.N <= 128;
+  if (!a7 && !a9) return false;
+  if (epi == EPI_BF16 && (p.N % 8 || p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15) || !p.out_bf16)) return false;
+  if (epi == EPI_F32 && (p.N % 8 || p.ldr % 4 || ((uintptr_t)p.out_f32 & 15) ||
+                         (p.out_bf16 && (p.ldo % 8 || ((uintptr_t)p.out_bf16 & 15)))))
+    return false;
+  return fits_rsrc(p) || p.conv;   // conv: gemm_launch splits past 2 GiB by whole images
+}
+
 hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
+  if (args.gn_part && !gemm_gn_fusable(args, epi)) return hipErrorInvalidValue;
   GemmArgs p = args;
   // tile order: groups of 8 row panels once there are >= 8 column tiles (an XCD's 32 resident tiles then share
   // 4 A and 8 W panels instead of 2 and 16); measured by tools/gemm_tune.py
@@ -3371,6 +3450,7 @@ hipError_t gemm_launch(const GemmArgs& args, int epi, hipStream_t stream) {
       if (b.res_f32) b.res_f32 += (size_t)m1 * p.ldrf;
       if (b.stats_out) b.stats_out += (size_t)m1 * p.stats_ld * 2;
       if (b.ln_stats) b.ln_stats += (size_t)m1 * p.ln_ld * 2;
+      if (b.gn_part) b.gn_part += (size_t)(m1 / p.gn_P) * (p.gn_P >> 8) * 64;   // whole images (conv split)
       hipError_t e = gemm_launch(a, epi, stream);
       if (e == hipSuccess) e = gemm_launch(b, epi, stream);
       if (e == hipSuccess && p.out2) e = out2_copy(p, stream);

@@ -88,6 +88,11 @@ struct GemmArgs {
   // 256 x 256 accumulator tile per workgroup).  Null: whole tiles only.
   unsigned* sk_flags;
   float* sk_slab;
+  // GroupNorm partials of the stored tile (the decoder's GroupNorm(32) inputs, libs/autoencoder.py Normalize): with
+  // gn_part the 256-tile epilogues (gemm8d, gemm8t; EPI_F32 / EPI_BF16) write, per 256-row chunk of an image of gn_P
+  // rows and per group of gn_cpg = N / 32 columns, the fp64 (sum, sum of squares) of the stored values to
+  // gn_part[((b * gn_P / 256 + chunk) * 32 + g) * 2 + {0,1}] -- gn_partial_kernel's layout with 256-pixel chunks
+  double* gn_part; int gn_P, gn_cpg;
 };
 void gemm_set_tuning(int raster, int dbg_tile0);
 // stream-K policy: 0 off (default), 1 auto (where the last wave of tiles is < 97 % full), 2 wherever it applies
@@ -96,6 +101,8 @@ int gemm_get_sk();
 long long gemm_sk_launches();
 int gemm_sk_stats(unsigned long long* out3);
 int gemm_seg_stats(unsigned long long* out25);
+// whether gemm_launch(p, epi) runs an epilogue that writes p.gn_part (the decoder falls back to gn_partial_kernel)
+bool gemm_gn_fusable(const GemmArgs& p, int epi);
 constexpr int SK_FLAG_WORDS = 256;                       // flags per launch
 constexpr long long SK_SLAB_BYTES = 256LL * 65536 * 4;   // 64 MiB
 

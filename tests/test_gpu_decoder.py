@@ -102,3 +102,27 @@ def test_decoder_rejects_unsupported(dev):
     ae, _ = _ae(32, (1, 2), 1, 13, "random", 8)
     with pytest.raises(ValueError):
         ae.to(dev).decode(torch.zeros(1, 4, 8, 8, device=dev))
+
+
+def test_decoder_gn_fusion_matches_separate_pass(dev):
+    """GroupNorm statistics taken in the producing conv / linear epilogues (GemmArgs::gn_part: 256-pixel chunks,
+    fp32 per thread, fp64 per group) vs the separate statistics pass (gn_partial_kernel).  They differ only in
+    summation order, but a bf16 activation chain 30 convolutions deep turns any such difference into a different
+    rounding pattern: the two decodes sit 0.9e-2 apart, each 1.1e-2 from the fp32 oracle (tools/gnf_probe.py,
+    profiles/r06g2).  So: both within the oracle tolerance, and the fused one no further from the oracle."""
+    from panopticdiffusionmodels_amd import _lib
+    lib = _lib.load()
+    ae, sd = _ae(128, (1, 2, 4, 4), 2, 21, "reference", 32)
+    ae = ae.to(dev)
+    g = torch.Generator().manual_seed(21)
+    z = torch.randn(2, 4, 32, 32, generator=g)
+    fused = ae.decode(z.to(dev)).cpu()
+    try:
+        assert lib.pdm_decoder_set_gn_fusion(0) == 0
+        sep = ae.decode(z.to(dev)).cpu()
+    finally:
+        lib.pdm_decoder_set_gn_fusion(1)
+    assert rel(fused, sep) < TOL
+    ref = autoencoder_ref.decode(sd, z[0:1])
+    assert rel(fused[0:1], ref) < TOL and rel(sep[0:1], ref) < TOL
+    assert rel(fused[0:1], ref) < 1.2 * rel(sep[0:1], ref)
