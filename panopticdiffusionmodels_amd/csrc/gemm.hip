@@ -1823,7 +1823,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
   const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
   int g = 0;                  // K-steps run so far: the ring slot of the next one is g & 1
-#ifdef PDM_G8S_SEG
+#if defined(PDM_G8S_SEG) || defined(PDM_G8S_ESEG)
   unsigned seg_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   bool pub_pending = false;   // SK: this workgroup's head slab stored, its flag not yet raised
@@ -2032,7 +2032,19 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       for (; kt + 2 < ke; ++kt, ++g) ktile(kt, STT{});
       for (; kt < ke; ++kt, ++g) ktile(kt, STF{});
     }
+#ifdef PDM_G8S_ESEG
+    // diagnostic builds only (-DPDM_G8S_ESEG, tools/g8s_eseg.py): shader cycles of the epilogue's parts per tile
+    unsigned long long eseg_t = __builtin_amdgcn_s_memtime();
+    auto eseg = [&](int i) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      seg_acc[i] += (unsigned)(t - eseg_t);
+      eseg_t = t;
+    };
+#else
+    auto eseg = [](int) {};
+#endif
     if (wave < 4) bar_raw();   // rejoin the stagger
+    eseg(0);
 
     if constexpr (SK) {
       if (kind == 1) {   // head: accumulators -> slab (sc1 write-through), the next tile's tables
@@ -2111,6 +2123,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
       for (int ni = 0; ni < 2; ++ni) {
         if (!ln || lnc) cs[qj][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
+    eseg(1);
     bar_raw();   // lnrow complete; the raw / column tables are free for the next tile's
     if constexpr (FP8) {
       if (lnc) {
@@ -2159,6 +2172,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
           mrow[qi][mi] = ln ? make_float2(mr8[qi * 4 + mi][0], mr8[qi * 4 + mi][1]) : make_float2(0.f, 1.f);
     }
 
+    eseg(2);
     if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
       unsigned e8[16];   // MXO: E8M0 scale of block (qi, mi, qj) at [qi * 8 + mi * 2 + qj]
 #pragma unroll
@@ -2307,6 +2321,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
           }
           rsum[qi][mi] = s2[0] + s2[1];
         }
+      eseg(3);
       // LayerNorm partials of the 256-column group (sum, M2 about the group mean): every wave reduces its own 64
       // columns of a row (sum over the 4 lane rows, M2 about the wave's own mean) and the 4 column waves (wn) are
       // merged with Chan's update through LDS -- one barrier.  Without stats_out the store still issues (to
@@ -2337,8 +2352,10 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
             if (g4 == 0) lds_wr64(tab + ((qi * 128 + wm * 64 + mi * 16 + r16) * 4 + wn) * 8, make_float2(sw, q));
           }
       }
+      eseg(4);
       lds_sync();
       bar_raw();
+      eseg(5);
       {   // one float per thread: row tid >> 1, component tid & 1 (sum, M2)
         const int tid_s = opaque_i(tid), ml = tid_s >> 1, c = tid_s & 1;
         f32x2 t4[4];
@@ -2359,7 +2376,9 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
         const unsigned off = (stats && m < M) ? (unsigned)((m * p.stats_ld + (n0 >> 8)) * 2 + c) * 4u : OOB;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), rst, (int)off, 0, 0);
       }
+      eseg(6);
     }
+    if constexpr (EPI != EPI_RES) eseg(6);
     m0 = m0n;
     n0 = n0n;
     kb = kbn;
@@ -2367,7 +2386,7 @@ __device__ __forceinline__ void gemm8s_body(const GemmArgs& p, int tiles_n, int 
     kind = kindn;
     if constexpr (GRP) cv = nv;
   }
-#ifdef PDM_G8S_SEG
+#if defined(PDM_G8S_SEG) || defined(PDM_G8S_ESEG)
   if (lane == 0 && (wave == 0 || wave == 4)) {
 #pragma unroll
     for (int i = 0; i < 12; ++i) atomicAdd(&g_seg_stats[(wave == 4 ? 12 : 0) + i], (unsigned long long)seg_acc[i]);
